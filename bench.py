@@ -1,0 +1,126 @@
+#!/usr/bin/env python3
+"""Headline benchmark: MLUPS of the d3q27 MRT channel flow at 512^3 (BASELINE.json).
+
+    python bench.py --gpus N --steps K --warmup W
+    torchrun --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
+
+One process per GPU.  The global lattice is 512^3 (strong scaling) unless --weak,
+decomposed in z-slabs with RCCL halo exchange overlapped with the interior kernel.
+Geometry: channel (bounce-back walls at y=0 and y=ny-1, reference zone "Channel"),
+MRT collision everywhere, body force ForceX; uniform initial state (synthetic case,
+as BASELINE.json prescribes).  Each timed step is the full reference iteration
+(collide-stream of every node + boundary + halo exchange; globals on the last step
+of the window, as Lattice::Iterate does).  Compute and storage precision: fp64
+(the reference default, src/configure.ac:208-211) unless --precision float.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+from tclb_amd.lattice import Lattice  # noqa: E402
+from tclb_amd.parallel.comm import init_distributed_from_env  # noqa: E402
+
+METRIC = "MLUPS (million lattice updates/sec) whole-node, d3q27 512^3, at 1/2/4/8 MI355X"
+
+
+def channel_flags(lat: Lattice) -> np.ndarray:
+    m = lat.model
+    mrt = m.node_type("MRT").value
+    wall = m.node_type("Wall").value
+    nx = lat.shape[0]
+    fl = np.full((lat.NZ, lat.NY, nx), mrt, dtype=np.uint32)
+    # global y of local rows (y is never split in 3-D)
+    fl[:, lat.gy + 0, :] = wall
+    fl[:, lat.gy + lat.shape[1] - 1, :] = wall
+    return fl.astype(np.uint16 if m.flag_bits == 16 else np.uint32)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--size", type=int, default=512)
+    ap.add_argument("--model", default="d3q27")
+    ap.add_argument("--precision", default="double", choices=["double", "float", "mixed"])
+    ap.add_argument("--weak", action="store_true", help="size^3 per GPU (z-extent x N)")
+    ap.add_argument("--block", default="0,0")
+    ap.add_argument("--no-overlap", action="store_true")
+    ap.add_argument("--cpu", action="store_true")
+    a = ap.parse_args()
+
+    use_gpu = torch.cuda.is_available() and not a.cpu
+    comm = init_distributed_from_env("cuda" if use_gpu else "cpu")
+    rank, world = comm.rank, comm.size
+    if use_gpu:
+        local = int(os.environ.get("LOCAL_RANK", "0"))
+        torch.cuda.set_device(local)
+        device = torch.device("cuda", local)
+    else:
+        device = torch.device("cpu")
+    n = a.size
+    shape = (n, n, n * world) if a.weak else (n, n, n)
+    bx, by = (int(v) for v in a.block.split(","))
+    lat = Lattice(a.model, shape, device=device, precision=a.precision, comm=comm, block=(bx, by),
+                  overlap=None if not a.no_overlap else False)
+    lat.set_flags(channel_flags(lat))
+    lat.set_setting("nu", 0.02)
+    lat.set_setting("ForceX", 1e-6)
+    lat.init()
+
+    def sync():
+        if use_gpu:
+            torch.cuda.synchronize()
+        comm.barrier()
+
+    lat.iterate(a.warmup, glob_last=False)
+    sync()
+    t0 = time.perf_counter()
+    lat.iterate(a.steps, glob_last=True)
+    sync()
+    dt = time.perf_counter() - t0
+    dt = comm.allreduce_scalar(dt, "max")
+    nodes = shape[0] * shape[1] * shape[2]
+    mlups = nodes * a.steps / dt / 1e6
+    ok = bool(np.isfinite(lat.globals.get("XFlux", 0.0)))
+    if rank == 0:
+        es = 8 if a.precision == "double" else 4
+        nf = lat.nf
+        bytes_node = 2 * nf * es + (2 if lat.model.flag_bits == 16 else 4)
+        out = {
+            "metric": METRIC,
+            "value": round(mlups, 2),
+            "unit": "MLUPS",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(dt / a.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak" if a.weak else "strong",
+            "vs_baseline": None,
+            "dtype": {"double": "fp64", "float": "fp32", "mixed": "fp64-compute/fp32-storage"}[a.precision],
+            "data": "synthetic (uniform init, channel walls + body force, random-free)",
+            "config": {"model": a.model, "global_batch": nodes, "seq_len": shape[0],
+                       "lattice": list(shape), "parallelism": f"zslab{world}" if world > 1 else "single",
+                       "device": "cuda" if use_gpu else "cpu"},
+            "effective_GBps_per_gpu": round(mlups * bytes_node / 1e3 / world, 1),
+            "globals_finite": ok,
+            "baseline_note": "reference publishes no MLUPS (BASELINE.md); vs_baseline null",
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,132 @@
+"""In-tree build driver: emit + compile every model for gfx950 (hipcc) and for the
+host (g++/OpenMP).  Replaces the reference's autoconf + generated makefiles
+(reference: makefile:1-20, src/makefile.main.Rt, src/makefile.Rt:56-118).
+
+Outputs go to ``tclb_amd/_build/lib/libtclb_<model>_{hip,cpu}.so`` (git-ignored but
+shipped to GPU boxes with the repo snapshot).  Rebuilds are skipped when the
+source hash of a target is unchanged.
+"""
+from __future__ import annotations
+
+import argparse
+import hashlib
+import os
+import shutil
+import subprocess
+import sys
+import time
+from concurrent.futures import ThreadPoolExecutor
+from typing import Dict, Iterable, List, Optional
+
+from .emit.emitter import BUILD, CSRC, emit_model
+from .models import registry
+
+LIB = os.path.join(BUILD, "lib")
+HIPCC = os.environ.get("TCLB_HIPCC", "/opt/rocm/bin/hipcc")
+CXX = os.environ.get("TCLB_CXX", "g++")
+ARCH = os.environ.get("TCLB_OFFLOAD_ARCH", "gfx950")
+
+
+def lib_path(model: str, kind: str) -> str:
+    return os.path.join(LIB, f"libtclb_{model}_{kind}.so")
+
+
+def _hash_inputs(paths: Iterable[str], extra: str = "") -> str:
+    h = hashlib.sha1(extra.encode())
+    for p in sorted(paths):
+        with open(p, "rb") as f:
+            h.update(p.encode())
+            h.update(f.read())
+    return h.hexdigest()
+
+
+def _deps(model_dir: str, dynamics: Optional[str]) -> List[str]:
+    inc = os.path.join(CSRC, "include", "tclb")
+    deps = [os.path.join(inc, f) for f in os.listdir(inc) if f.endswith((".hpp", ".h"))]
+    deps += [os.path.join(model_dir, f) for f in os.listdir(model_dir) if f.endswith((".hpp", ".hip", ".cpp"))]
+    if dynamics:
+        deps.append(os.path.join(CSRC, "models", dynamics))
+    return deps
+
+
+def _cmd(kind: str, src: str, out: str, gen_dir: str) -> List[str]:
+    incs = ["-I", os.path.join(CSRC, "include"), "-I", os.path.join(CSRC, "models"), "-I", gen_dir]
+    if kind == "hip":
+        return [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
+                "-munsafe-fp-atomics", "-Wno-unused-result", "-Wno-pass-failed", *incs, src, "-o", out]
+    return [CXX, "-O3", "-std=c++17", "-fPIC", "-shared", "-fopenmp", "-fno-strict-aliasing",
+            "-Wno-unused-variable", *incs, src, "-o", out]
+
+
+def build_model(name: str, kinds=("cpu", "hip"), force: bool = False, verbose: bool = False) -> Dict[str, str]:
+    model = registry.get(name)
+    paths = emit_model(model)
+    os.makedirs(LIB, exist_ok=True)
+    out = {}
+    for kind in kinds:
+        if kind == "hip" and not os.path.exists(HIPCC):
+            continue
+        target = lib_path(name, kind)
+        src = paths[kind]
+        cmd = _cmd(kind, src, target, paths["dir"])
+        h = _hash_inputs(_deps(paths["dir"], model.dynamics), " ".join(cmd))
+        stamp = target + ".hash"
+        if not force and os.path.exists(target) and os.path.exists(stamp) and open(stamp).read() == h:
+            out[kind] = target
+            continue
+        t0 = time.time()
+        tmp = target + ".tmp"
+        cmd[-1] = tmp
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"build of {name} [{kind}] failed:\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr[-20000:]}")
+        os.replace(tmp, target)
+        with open(stamp, "w") as f:
+            f.write(h)
+        if verbose:
+            print(f"[tclb build] {name} [{kind}] {time.time() - t0:.1f}s", flush=True)
+        out[kind] = target
+    return out
+
+
+def build_all(models: Optional[List[str]] = None, kinds=("cpu", "hip"), jobs: int = 0, force=False,
+              verbose=False) -> Dict[str, Dict[str, str]]:
+    models = models or registry.names()
+    jobs = jobs or max(1, min(8, os.cpu_count() or 1))
+    tasks = [(m, k) for m in models for k in kinds]
+    res: Dict[str, Dict[str, str]] = {m: {} for m in models}
+    # emit serially (sympy + file writes), compile in parallel
+    for m in models:
+        emit_model(registry.get(m))
+    errors = []
+
+    def one(t):
+        m, k = t
+        try:
+            return m, k, build_model(m, kinds=(k,), force=force, verbose=verbose).get(k), None
+        except Exception as e:  # noqa
+            return m, k, None, e
+
+    with ThreadPoolExecutor(max_workers=jobs) as ex:
+        for m, k, p, e in ex.map(one, tasks):
+            if e is not None:
+                errors.append(e)
+            elif p:
+                res[m][k] = p
+    if errors:
+        raise RuntimeError("\n\n".join(str(e) for e in errors))
+    return res
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser(description="build tclb_amd model kernels")
+    ap.add_argument("models", nargs="*")
+    ap.add_argument("--kinds", default="cpu,hip")
+    ap.add_argument("-j", "--jobs", type=int, default=0)
+    ap.add_argument("--force", action="store_true")
+    a = ap.parse_args(argv)
+    build_all(a.models or None, kinds=tuple(a.kinds.split(",")), jobs=a.jobs, force=a.force, verbose=True)
+
+
+if __name__ == "__main__":
+    main()

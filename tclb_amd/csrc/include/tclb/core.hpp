@@ -1,0 +1,98 @@
+// tclb_amd — core device/host definitions shared by every model kernel.
+//
+// One source, two drivers: every model's node code is compiled once by hipcc for
+// gfx950 (GPU executor, see executor_hip.hpp) and once by g++ (OpenMP CPU executor,
+// see executor_cpu.hpp).  This replaces the reference's cross.h CUDA/HIP/CPU macro
+// shim (reference: src/cross.h:57-346) with two explicit executors and no CUDA path.
+#pragma once
+#include <stdint.h>
+#include <math.h>
+#include <stddef.h>
+
+#if defined(__HIPCC__)
+#include <hip/hip_runtime.h>
+#define TCLB_FN __host__ __device__ __forceinline__
+#define TCLB_DEV __device__ __forceinline__
+#define TCLB_GPU 1
+#else
+#define TCLB_FN inline
+#define TCLB_DEV inline
+#define TCLB_GPU 0
+#endif
+
+#define TCLB_UNROLL _Pragma("unroll")
+
+namespace tclb {
+
+typedef uint32_t flag_t;  // node type word (reference: flag_t 16/32 bit, src/conf.R:620-628)
+
+template <class R>
+struct vec3 {
+  R x, y, z;
+};
+
+// Launch descriptor.  POD, mirrored field-for-field by tclb_amd/ops/abi.py (ctypes).
+// Layout of one snapshot: storage_t[nfields][nz+2gz][ny+2gy][px], x fastest (SoA, like
+// the reference's field-major margin blocks, src/conf.R:952-957) but with contiguous
+// ghost planes on the decomposed axis instead of 27 margin blocks.
+struct Launch {
+  const void* in;          // input snapshot base
+  void* out;               // output snapshot base
+  const void* flags;       // flag_t, same node indexing as one field (incl. ghosts)
+  const double* settings;  // [NSETTINGS] global settings
+  const double* zonal;     // [NZSETTINGS][nzones]
+  double* globals;         // [NGLOBALS] accumulators (atomic)
+  void* aux;               // quantity output / misc pointer
+  void* stream;            // hipStream_t (GPU) or unused
+  long long sy, sz, fs;    // strides: y, z, field (elements)
+  int nx, ny, nz, px;      // local interior size + x pitch
+  int gy, gz;              // ghost depth along y / z
+  int x0, y0, z0;          // global offset of local (0,0,0)
+  int gnx, gny, gnz;       // global lattice size
+  int xlo, xhi, ylo, yhi, zlo, zhi;  // box of nodes to process (local coords)
+  int iter;                // iteration counter (Time)
+  int nzones;              // zone pitch of the zonal table
+  int stage;               // stage index (see model meta)
+  int glob;                // 0: no globals, 1: integrate globals
+  int quantity;            // quantity index for get-quantity launches
+  int qcomp;               // component stride of vector quantities (elements)
+  double qscale;           // unit scale for quantity output
+  long long qsy, qsz;      // quantity buffer strides (box-relative)
+  int block_x, block_y;    // launch shape hint (GPU)
+  int reserved0, reserved1;
+};
+
+// Periodic wrap helper for non-decomposed axes.
+TCLB_FN int wrap(int v, int n) { return v < 0 ? v + n : (v >= n ? v - n : v); }
+
+// ---------------------------------------------------------------------------
+// Node addressing.  Offsets inside one field are 32-bit (a field is < 2^31
+// elements: 1290^3 nodes); field bases are uniform 64-bit values so that loads
+// lower to SGPR-base + VGPR-offset addressing on gfx950.
+// ---------------------------------------------------------------------------
+struct Addr {
+  int x, y, z;  // local coordinates
+  int node;     // offset of (x,y,z) inside a field
+  int nx, ny, nz, gy, gz, sy, sz;
+  TCLB_FN void init(const Launch& L, int x_, int y_, int z_) {
+    x = x_; y = y_; z = z_;
+    nx = L.nx; ny = L.ny; nz = L.nz; gy = L.gy; gz = L.gz;
+    sy = (int)L.sy; sz = (int)L.sz;
+    node = x + sy * (y + gy) + sz * (z + gz);
+  }
+  TCLB_FN int off(int dx, int dy, int dz) const {
+    int xx = dx == 0 ? x : wrap(x + dx, nx);
+    int yy = y + dy;
+    if (dy != 0 && gy == 0) yy = wrap(yy, ny);
+    int zz = z + dz;
+    if (dz != 0 && gz == 0) zz = wrap(zz, nz);
+    return xx + sy * (yy + gy) + sz * (zz + gz);
+  }
+};
+
+template <class T>
+TCLB_FN T tmax(T a, T b) { return a > b ? a : b; }
+template <class T>
+TCLB_FN T tmin(T a, T b) { return a < b ? a : b; }
+
+}  // namespace tclb

@@ -1,0 +1,173 @@
+// GPU executor for gfx950 (MI355X): one thread per lattice node, wave64 rows.
+//
+// Replaces the reference's Kernel<InteriorExecutor/BorderExecutor> (reference:
+// src/LatticeContainer.inc.cpp.Rt:201-287; block 32x4 with WARPSIZE=32 even on HIP)
+// with CDNA4-shaped launches: blocks are (BX x BY) with BX a multiple of 64 so that
+// every wavefront covers 64 consecutive x-nodes (one fully coalesced 512 B fp64 row
+// segment per population); the border/interior split is expressed by the caller as a
+// z- (or y-) range of the same kernel so it can run on separate HIP streams.
+// Globals are reduced wave64 -> LDS -> one atomic per block and global
+// (reference: per-warp(32) reduce + atomics, src/cuda.cu.Rt:93-179).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <utility>
+#include "core.hpp"
+
+namespace tclb {
+namespace exec {
+
+template <class R>
+__device__ __forceinline__ R wave_sum(R v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+template <class R>
+__device__ __forceinline__ R wave_max(R v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    R w = __shfl_xor(v, o, 64);
+    v = v > w ? v : w;
+  }
+  return v;
+}
+
+__device__ __forceinline__ void atomic_max_double(double* addr, double v) {
+  unsigned long long* a = (unsigned long long*)addr;
+  unsigned long long old = __hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  while (__longlong_as_double(old) < v) {
+    unsigned long long assumed = old;
+    old = atomicCAS(a, assumed, (unsigned long long)__double_as_longlong(v));
+    if (old == assumed) break;
+  }
+}
+
+// Reduce per-thread accumulators g[NG] of a block and add into dst (device, double).
+template <int NG, int NSUM, class R>
+__device__ __forceinline__ void block_globals(R* g, double* dst) {
+  __shared__ double part[NG][16];
+  const int tid = threadIdx.x + blockDim.x * threadIdx.y;
+  const int lane = tid & 63, wid = tid >> 6;
+  const int nw = (blockDim.x * blockDim.y + 63) >> 6;
+#pragma unroll
+  for (int i = 0; i < NG; i++) {
+    R v = i < NSUM ? wave_sum(g[i]) : wave_max(g[i]);
+    if (lane == 0) part[i][wid] = (double)v;
+  }
+  __syncthreads();
+  if (tid < NG) {
+    double acc = part[tid][0];
+    for (int w = 1; w < nw; w++) acc = tid < NSUM ? acc + part[tid][w] : (acc > part[tid][w] ? acc : part[tid][w]);
+    if (tid < NSUM) {
+      if (acc != 0.0) unsafeAtomicAdd(dst + tid, acc);
+    } else {
+      atomic_max_double(dst + tid, acc);
+    }
+  }
+}
+
+template <class Model, class R, class S, int STG, bool GLOB>
+__global__ void __launch_bounds__(256) k_stage(const Launch L) {
+  const int x = L.xlo + (int)(blockIdx.x * blockDim.x + threadIdx.x);
+  const int y = L.ylo + (int)(blockIdx.y * blockDim.y + threadIdx.y);
+  const int z = L.zlo + (int)blockIdx.z;
+  constexpr int NG = GLOB ? Model::NGLOBALS_ : 1;
+  R g[NG];
+#pragma unroll
+  for (int i = 0; i < NG; i++) g[i] = i < Model::NSUMGLOBALS_ ? R(0) : R(-1e30);
+  if (x < L.xhi && y < L.yhi) {
+    typename Model::template NodeT<R, S, GLOB> n(L, x, y, z, g);
+    n.template run_stage<STG>();
+  }
+  if constexpr (GLOB) block_globals<NG, Model::NSUMGLOBALS_>(g, L.globals);
+}
+
+template <class Model, class R, class S>
+__global__ void __launch_bounds__(256) k_quantity(const Launch L) {
+  const int x = L.xlo + (int)(blockIdx.x * blockDim.x + threadIdx.x);
+  const int y = L.ylo + (int)(blockIdx.y * blockDim.y + threadIdx.y);
+  const int z = L.zlo + (int)blockIdx.z;
+  if (x >= L.xhi || y >= L.yhi) return;
+  R g[1];
+  typename Model::template NodeT<R, S, false> n(L, x, y, z, g);
+  n.pop();
+  R o[3] = {R(0), R(0), R(0)};
+  n.get_quantity(L.quantity, o);
+  const long long idx = (long long)(x - L.xlo) + L.qsy * (y - L.ylo) + L.qsz * (z - L.zlo);
+  R* out = (R*)L.aux;
+  const int nc = L.reserved0 > 0 ? L.reserved0 : 1;
+  for (int c = 0; c < nc; c++) out[idx + (long long)c * L.qcomp] = o[c] * R(L.qscale);
+}
+
+inline void launch_shape(const Launch& L, dim3& grid, dim3& block) {
+  const int w = L.xhi - L.xlo, h = L.yhi - L.ylo, d = L.zhi - L.zlo;
+  int bx = L.block_x > 0 ? L.block_x : 0;
+  if (bx == 0) {
+    bx = 64;
+    while (bx < 256 && bx < w) bx *= 2;
+  }
+  int by = L.block_y > 0 ? L.block_y : 256 / bx;
+  if (by < 1) by = 1;
+  block = dim3(bx, by, 1);
+  grid = dim3((w + bx - 1) / bx, (h + by - 1) / by, d);
+}
+
+template <class Model, class R, class S, int I, bool G>
+inline bool launch_one(const Launch& L, dim3 grid, dim3 block, hipStream_t s) {
+  k_stage<Model, R, S, I, G><<<grid, block, 0, s>>>(L);
+  return true;
+}
+
+template <class Model, class R, class S, bool G, int... I>
+inline int run_stage_impl(const Launch& L, std::integer_sequence<int, I...>) {
+  dim3 grid, block;
+  launch_shape(L, grid, block);
+  if (grid.x == 0 || grid.y == 0 || grid.z == 0) return 0;
+  hipStream_t s = (hipStream_t)L.stream;
+  bool found = false;
+  ((L.stage == I ? (found = launch_one<Model, R, S, I, G>(L, grid, block, s)) : false), ...);
+  if (!found) return -2;
+  return (int)hipGetLastError();
+}
+
+template <class Model, class R, class S>
+inline int run_stage(const Launch& L) {
+  using Seq = std::make_integer_sequence<int, Model::NSTAGES_>;
+  if (L.glob) return run_stage_impl<Model, R, S, true>(L, Seq{});
+  return run_stage_impl<Model, R, S, false>(L, Seq{});
+}
+
+template <class Model, class R, class S>
+inline int run_quantity(const Launch& L) {
+  dim3 grid, block;
+  launch_shape(L, grid, block);
+  if (grid.x == 0 || grid.y == 0 || grid.z == 0) return 0;
+  k_quantity<Model, R, S><<<grid, block, 0, (hipStream_t)L.stream>>>(L);
+  return (int)hipGetLastError();
+}
+
+}  // namespace exec
+}  // namespace tclb
+
+// C ABI: prec 0 = fp64 compute / fp64 storage (reference default, src/configure.ac:208-211)
+//        prec 1 = fp32 compute / fp32 storage
+//        prec 2 = fp64 compute / fp32 storage (reference --with-storage=float)
+#define TCLB_EXPORT_MODEL(NAME, MODEL)                                                       \
+  extern "C" int tclb_##NAME##_run(const tclb::Launch* L, int prec) {                        \
+    switch (prec) {                                                                          \
+      case 0: return tclb::exec::run_stage<MODEL, double, double>(*L);                       \
+      case 1: return tclb::exec::run_stage<MODEL, float, float>(*L);                         \
+      case 2: return tclb::exec::run_stage<MODEL, double, float>(*L);                        \
+      default: return -1;                                                                    \
+    }                                                                                        \
+  }                                                                                          \
+  extern "C" int tclb_##NAME##_quantity(const tclb::Launch* L, int prec) {                   \
+    switch (prec) {                                                                          \
+      case 0: return tclb::exec::run_quantity<MODEL, double, double>(*L);                    \
+      case 1: return tclb::exec::run_quantity<MODEL, float, float>(*L);                      \
+      case 2: return tclb::exec::run_quantity<MODEL, double, float>(*L);                     \
+      default: return -1;                                                                    \
+    }                                                                                        \
+  }                                                                                          \
+  extern "C" int tclb_##NAME##_device() { return 1; }                                        \
+  extern "C" int tclb_##NAME##_sizeof_launch() { return (int)sizeof(tclb::Launch); }

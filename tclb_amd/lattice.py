@@ -1,0 +1,406 @@
+"""Lattice runtime: snapshots, settings, zones, stages/actions, halos, globals.
+
+MI355X-native re-design of the reference's ``Lattice`` (reference: src/Lattice.h.Rt:39-191,
+src/Lattice.cu.Rt).  Differences by design:
+
+* A snapshot is ONE device tensor ``[nfields][nz+2g][ny][px]`` (SoA, x fastest, x
+  pitch padded to 64 elements = 512 B rows in fp64) with contiguous ghost planes on
+  the decomposed axis, instead of 27 margin blocks per snapshot.
+* Settings live in a small device array read through the scalar cache (no
+  ``__constant__`` re-upload per launch, cf. CopyToConst src/LatticeContainer.inc.cpp.Rt:294).
+* A stage is one kernel over a box; with >1 rank the box is split into border planes
+  and interior so that the halo exchange (RCCL P2P over xGMI) overlaps the interior
+  kernel (reference: RunBorder -> MPIStream_A -> RunInterior -> MPIStream_B,
+  src/Lattice.cu.Rt:466-533).
+* Globals: device fp64 accumulators, all-reduced (SUM then MAX) across ranks
+  (reference: MPI_Reduce to rank 0, src/Lattice.cu.Rt:1279-1315).
+"""
+from __future__ import annotations
+
+import math
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+
+from .models import registry
+from .models.dsl import Model
+from .ops import abi
+from .parallel.comm import Comm, LoopbackComm
+from .parallel.decomp import Slab, decompose
+
+_SAFE_MATH = {k: getattr(math, k) for k in ("sqrt", "exp", "log", "sin", "cos", "tan", "atan", "atan2", "pi",
+                                              "pow", "fabs", "floor", "ceil", "tanh", "sinh", "cosh", "acos", "asin")}
+_SAFE_MATH["abs"] = abs
+_SAFE_MATH["min"] = min
+_SAFE_MATH["max"] = max
+
+
+def eval_expr(expr: str, env: Dict[str, float]) -> float:
+    return float(eval(expr, {"__builtins__": {}}, {**_SAFE_MATH, **env}))
+
+
+def _runs(idx: Sequence[int]) -> List[Tuple[int, int]]:
+    """contiguous runs [a, b) of a sorted index list"""
+    out = []
+    for i in sorted(idx):
+        if out and out[-1][1] == i:
+            out[-1][1] = i + 1
+        else:
+            out.append([i, i + 1])
+    return [(a, b) for a, b in out]
+
+
+class Lattice:
+    def __init__(self, model, shape: Tuple[int, int, int], device: Optional[torch.device] = None,
+                 precision: str = "double", comm: Optional[Comm] = None, block: Tuple[int, int] = (0, 0),
+                 overlap: Optional[bool] = None):
+        self.model: Model = registry.get(model) if isinstance(model, str) else model.finalize()
+        m = self.model
+        self.comm = comm or LoopbackComm()
+        gnx, gny, gnz = (list(shape) + [1, 1])[:3]
+        if m.dims == 2 and gnz != 1:
+            raise ValueError(f"2-D model {m.name} needs nz=1")
+        self.gshape = (gnx, gny, gnz)
+        hx, hy, hz = m.halo()
+        self.slab: Slab = decompose(gnx, gny, gnz, self.comm.rank, self.comm.size, halo=max(1, hz if gnz > 1 else hy))
+        ax = self.slab.axis
+        self.g = max(1, hz if ax == 2 else hy)
+        nx, ny, nz = self.slab.local_shape
+        self.shape = (nx, ny, nz)
+        self.gy = self.g if ax == 1 else 0
+        self.gz = self.g if ax == 2 else 0
+        if ax == 2 and hy > ny:
+            raise ValueError("y stencil larger than domain")
+        self.px = ((nx + 63) // 64) * 64 if nx >= 64 else ((nx + 7) // 8) * 8
+        self.NY = ny + 2 * self.gy
+        self.NZ = nz + 2 * self.gz
+        self.device = torch.device(device) if device is not None else torch.device("cpu")
+        self.is_gpu = self.device.type == "cuda"
+        self.precision = precision
+        self.prec = abi.PREC[precision]
+        self.sdtype = torch.float32 if precision in ("float", "mixed") else torch.float64
+        self.rdtype = torch.float32 if precision == "float" else torch.float64
+        nf = len(m.fields)
+        self.nf = nf
+        self.fs = self.NZ * self.NY * self.px
+        if self.fs >= 2 ** 31:
+            raise ValueError("local field exceeds 2^31 elements; use more ranks")
+        self.snaps = [torch.zeros((nf, self.NZ, self.NY, self.px), dtype=self.sdtype, device=self.device)
+                      for _ in range(2)]
+        self.cur = 0
+        fdt = torch.int16 if m.flag_bits == 16 else torch.int32
+        self.flags = torch.zeros((self.NZ, self.NY, self.px), dtype=fdt, device=self.device)
+        # settings
+        self.gsettings = [s.name for s in m.global_settings]
+        self.zsettings = [s.name for s in m.zonal_settings]
+        self.svals = np.zeros(max(1, len(self.gsettings)), dtype=np.float64)
+        self.zone_names: Dict[str, int] = {"DefaultZone": 0}
+        self.zvals = np.zeros((max(1, len(self.zsettings)), 1), dtype=np.float64)
+        self._settings_dirty = True
+        self.settings_t = torch.zeros(self.svals.shape, dtype=torch.float64, device=self.device)
+        self.zonal_t = torch.zeros(self.zvals.size, dtype=torch.float64, device=self.device)
+        self.globals_t = torch.zeros(max(1, len(m.globals_)), dtype=torch.float64, device=self.device)
+        self.globals: Dict[str, float] = {g.name: 0.0 for g in m.globals_}
+        self.iter = 0
+        self.block = block
+        self.overlap = self.comm.distributed if overlap is None else overlap
+        kind = "hip" if self.is_gpu else "cpu"
+        self.lib = abi.load(m.name, kind)
+        # halo field sets: fields read from below (stencil min < 0) / above (max > 0) along axis
+        self.halo_lo = [i for i, f in enumerate(m.fields) if f.stencil[ax][0] < 0]
+        self.halo_hi = [i for i, f in enumerate(m.fields) if f.stencil[ax][1] > 0]
+        self._halo_bufs = {}
+        for s in m.settings:
+            self.set_setting(s.name, s.default, _init=True)
+        self._L = self._base_launch()
+        self.callbacks = []
+
+    # ------------------------------------------------------------------ launch
+    def _base_launch(self) -> abi.Launch:
+        L = abi.Launch()
+        nx, ny, nz = self.shape
+        L.sy = self.px
+        L.sz = self.px * self.NY
+        L.fs = self.fs
+        L.nx, L.ny, L.nz, L.px = nx, ny, nz, self.px
+        L.gy, L.gz = self.gy, self.gz
+        ox, oy, oz = self.slab.offset
+        L.x0, L.y0, L.z0 = ox, oy, oz
+        L.gnx, L.gny, L.gnz = self.gshape
+        L.xlo, L.xhi, L.ylo, L.yhi, L.zlo, L.zhi = 0, nx, 0, ny, 0, nz
+        L.block_x, L.block_y = self.block
+        L.flags = self.flags.data_ptr()
+        return L
+
+    def _sync_settings(self):
+        if self._settings_dirty:
+            self.settings_t = torch.as_tensor(self.svals, dtype=torch.float64).to(self.device)
+            self.zonal_t = torch.as_tensor(np.ascontiguousarray(self.zvals).reshape(-1), dtype=torch.float64).to(self.device)
+            self._settings_dirty = False
+        L = self._L
+        L.settings = self.settings_t.data_ptr()
+        L.zonal = self.zonal_t.data_ptr()
+        L.nzones = self.zvals.shape[1]
+        L.globals_ = self.globals_t.data_ptr()
+        L.flags = self.flags.data_ptr()
+
+    def _stream(self) -> int:
+        return torch.cuda.current_stream(self.device).cuda_stream if self.is_gpu else 0
+
+    def _launch_stage(self, stage: int, src: torch.Tensor, dst: torch.Tensor, glob: bool,
+                      axis_range: Optional[Tuple[int, int]] = None):
+        L = self._L
+        L.in_ = src.data_ptr()
+        L.out = dst.data_ptr()
+        L.stage = stage
+        L.glob = 1 if glob else 0
+        L.iter = self.iter
+        L.stream = self._stream()
+        nx, ny, nz = self.shape
+        L.ylo, L.yhi, L.zlo, L.zhi = 0, ny, 0, nz
+        if axis_range is not None:
+            if self.slab.axis == 2:
+                L.zlo, L.zhi = axis_range
+            else:
+                L.ylo, L.yhi = axis_range
+        self.lib.run(L, self.prec)
+
+    # ------------------------------------------------------------------ halos
+    def _axis_planes(self, buf: torch.Tensor, a: int, b: int) -> torch.Tensor:
+        """view of planes [a, b) in ghost-inclusive coordinates along the decomposed axis"""
+        return buf[:, a:b] if self.slab.axis == 2 else buf[:, :, a:b]
+
+    def _pack(self, buf: torch.Tensor, fields: List[int], a: int, b: int) -> torch.Tensor:
+        planes = self._axis_planes(buf, a, b)
+        runs = _runs(fields)
+        if len(runs) == 1:
+            return planes[runs[0][0]:runs[0][1]].contiguous()
+        return torch.cat([planes[r0:r1] for r0, r1 in runs], 0).contiguous()
+
+    def _unpack(self, buf: torch.Tensor, fields: List[int], a: int, b: int, data: torch.Tensor):
+        planes = self._axis_planes(buf, a, b)
+        k = 0
+        for r0, r1 in _runs(fields):
+            planes[r0:r1].copy_(data[k:k + (r1 - r0)])
+            k += r1 - r0
+
+    def _halo_start(self, buf: torch.Tensor, fields: Optional[Sequence[int]] = None):
+        g = self.g
+        n = self.shape[2] if self.slab.axis == 2 else self.shape[1]
+        lo = [i for i in self.halo_lo if fields is None or i in fields]
+        hi = [i for i in self.halo_hi if fields is None or i in fields]
+        if not self.comm.distributed:
+            # loopback: periodic wrap = plane copies inside this snapshot
+            for r0, r1 in _runs(lo):
+                self._axis_planes(buf, 0, g)[r0:r1].copy_(self._axis_planes(buf, n, n + g)[r0:r1])
+            for r0, r1 in _runs(hi):
+                self._axis_planes(buf, n + g, n + 2 * g)[r0:r1].copy_(self._axis_planes(buf, g, 2 * g)[r0:r1])
+            return None
+        send_up = self._pack(buf, lo, n, n + g) if lo else None        # my top planes -> next's lower ghost
+        send_down = self._pack(buf, hi, g, 2 * g) if hi else None      # my bottom planes -> prev's upper ghost
+        recv_below = torch.empty_like(send_up) if lo else None
+        recv_above = torch.empty_like(send_down) if hi else None
+        h = self.comm.start_halo(send_up, send_down, recv_below, recv_above)
+        return (h, buf, lo, hi, recv_below, recv_above, send_up, send_down)
+
+    def _halo_finish(self, st):
+        if st is None:
+            return
+        h, buf, lo, hi, rb, ra, su, sd = st
+        self.comm.wait_halo(h)
+        g = self.g
+        n = self.shape[2] if self.slab.axis == 2 else self.shape[1]
+        if lo:
+            self._unpack(buf, lo, 0, g, rb)
+        if hi:
+            self._unpack(buf, hi, n + g, n + 2 * g, ra)
+
+    def exchange(self, buf: Optional[torch.Tensor] = None, fields=None):
+        buf = self.snaps[self.cur] if buf is None else buf
+        self._halo_finish(self._halo_start(buf, fields))
+
+    # ------------------------------------------------------------------ actions
+    def _saved_fields(self, stage) -> List[int]:
+        if stage.save_fields is None:
+            return list(range(self.nf))
+        return [i for i, f in enumerate(self.model.fields) if f.nicename in stage.save_fields or f.name in stage.save_fields]
+
+    def run_action(self, name: str, glob: bool = False):
+        m = self.model
+        act = m.action(name)
+        if act is None:
+            raise KeyError(f"model {m.name} has no action {name}")
+        self._sync_settings()
+        src = self.snaps[self.cur]
+        dst = self.snaps[1 - self.cur]
+        if glob:
+            self.globals_t.zero_()
+        n = self.shape[2] if self.slab.axis == 2 else self.shape[1]
+        g = self.g
+        for k, sname in enumerate(act.stages):
+            si = m.stage_index(sname)
+            st = m.stage(sname)
+            inp = src if k == 0 else dst
+            fields = self._saved_fields(st)
+            if self.overlap and n > 2 * g:
+                self._launch_stage(si, inp, dst, glob, (0, g))
+                self._launch_stage(si, inp, dst, glob, (n - g, n))
+                hs = self._halo_start(dst, fields)
+                self._launch_stage(si, inp, dst, glob, (g, n - g))
+                self._halo_finish(hs)
+            else:
+                self._launch_stage(si, inp, dst, glob)
+                self._halo_finish(self._halo_start(dst, fields))
+        self.cur = 1 - self.cur
+        if glob:
+            self._reduce_globals()
+
+    def _reduce_globals(self):
+        g = self.comm.allreduce_globals(self.globals_t, self.model.n_sum_globals)
+        vals = g.detach().cpu().numpy()
+        for i, gl in enumerate(self.model.globals_):
+            self.globals[gl.name] = float(vals[i])
+
+    def init(self):
+        """Action Init (reference: Lattice::Init -> Action_Init, src/Lattice.cu.Rt:799-821)."""
+        self.iter = 0
+        self.run_action("Init", glob=False)
+
+    def iterate(self, n: int, glob_last: bool = True, action: str = "Iteration"):
+        """Reference Lattice::Iterate (src/Lattice.cu.Rt:900-989): globals on the last step."""
+        for i in range(n):
+            glob = glob_last and i == n - 1
+            self.run_action(action, glob=glob)
+            self.iter += 1
+            for cb in self.callbacks:
+                cb(self)
+
+    # ------------------------------------------------------------------ settings
+    def set_setting(self, name: str, value: float, zone: Optional[str] = None, _init: bool = False):
+        m = self.model
+        s = m.setting(name)
+        if s is None:
+            raise KeyError(f"model {m.name} has no setting {name}")
+        value = float(value)
+        if s.zonal:
+            zi = self.zsettings.index(name)
+            if zone is None:
+                self.zvals[zi, :] = value
+            else:
+                self.zvals[zi, self.zone_index(zone)] = value
+        else:
+            self.svals[self.gsettings.index(name)] = value
+        self._settings_dirty = True
+        if s.derived:
+            env = self.settings_dict(zone)
+            env[name] = value
+            for tgt, expr in s.derived.items():
+                self.set_setting(tgt, eval_expr(expr, env), zone=zone)
+
+    def get_setting(self, name: str, zone: Optional[str] = None) -> float:
+        s = self.model.setting(name)
+        if s is None:
+            raise KeyError(name)
+        if s.zonal:
+            return float(self.zvals[self.zsettings.index(name), self.zone_index(zone or "DefaultZone")])
+        return float(self.svals[self.gsettings.index(name)])
+
+    def settings_dict(self, zone: Optional[str] = None) -> Dict[str, float]:
+        d = {n: float(self.svals[i]) for i, n in enumerate(self.gsettings)}
+        zi = self.zone_index(zone) if zone is not None and zone in self.zone_names else 0
+        for i, n in enumerate(self.zsettings):
+            d[n] = float(self.zvals[i, zi])
+        return d
+
+    def zone_index(self, zone: str) -> int:
+        if zone not in self.zone_names:
+            self.add_zone(zone)
+        return self.zone_names[zone]
+
+    def add_zone(self, zone: str) -> int:
+        if zone in self.zone_names:
+            return self.zone_names[zone]
+        zi = len(self.zone_names)
+        if zi > self.model.zone_max:
+            raise ValueError(f"too many zones for model {self.model.name} (max {self.model.zone_max})")
+        self.zone_names[zone] = zi
+        col = self.zvals[:, :1]
+        self.zvals = np.concatenate([self.zvals, col], axis=1)
+        self._settings_dirty = True
+        return zi
+
+    # ------------------------------------------------------------------ flags
+    def set_flags(self, flags: np.ndarray):
+        """flags: (NZ, NY, nx) incl. ghost planes along the decomposed axis"""
+        nx = self.shape[0]
+        full = np.zeros((self.NZ, self.NY, self.px), dtype=np.uint16 if self.model.flag_bits == 16 else np.uint32)
+        full[:, :, :nx] = flags
+        view = full.view(np.int16 if self.model.flag_bits == 16 else np.int32)
+        self.flags.copy_(torch.from_numpy(view))
+
+    def get_flags(self) -> np.ndarray:
+        """interior flags (nz, ny, nx) as unsigned"""
+        f = self.flags.cpu().numpy()
+        f = f.view(np.uint16 if self.model.flag_bits == 16 else np.uint32)
+        return self._interior(f)
+
+    def _interior(self, a):
+        nx, ny, nz = self.shape
+        return a[self.gz:self.gz + nz, self.gy:self.gy + ny, :nx]
+
+    # ------------------------------------------------------------------ fields / quantities
+    def field(self, name: str) -> torch.Tensor:
+        """interior view of a stored field in the current snapshot: (nz, ny, nx)"""
+        i = self.model.field_index(name)
+        nx, ny, nz = self.shape
+        return self.snaps[self.cur][i, self.gz:self.gz + nz, self.gy:self.gy + ny, :nx]
+
+    def fields_interior(self) -> torch.Tensor:
+        nx, ny, nz = self.shape
+        return self.snaps[self.cur][:, self.gz:self.gz + nz, self.gy:self.gy + ny, :nx]
+
+    def set_fields_interior(self, data: torch.Tensor):
+        nx, ny, nz = self.shape
+        self.snaps[self.cur][:, self.gz:self.gz + nz, self.gy:self.gy + ny, :nx].copy_(data)
+        self.exchange()
+
+    def quantity(self, name: str, scale: float = 1.0) -> torch.Tensor:
+        """compute a quantity over the local interior: returns (ncomp, nz, ny, nx)"""
+        m = self.model
+        qi = next((i for i, q in enumerate(m.quantities) if q.name == name), None)
+        if qi is None:
+            raise KeyError(f"model {m.name} has no quantity {name}")
+        q = m.quantities[qi]
+        nc = 3 if q.vector else 1
+        nx, ny, nz = self.shape
+        out = torch.empty((nc, nz, ny, nx), dtype=self.rdtype, device=self.device)
+        self._sync_settings()
+        L = self._L
+        L.in_ = self.snaps[self.cur].data_ptr()
+        L.out = self.snaps[1 - self.cur].data_ptr()
+        L.aux = out.data_ptr()
+        L.quantity = qi
+        L.qcomp = nx * ny * nz
+        L.qscale = float(scale)
+        L.qsy = nx
+        L.qsz = nx * ny
+        L.reserved0 = nc
+        L.ylo, L.yhi, L.zlo, L.zhi = 0, ny, 0, nz
+        L.iter = self.iter
+        L.stream = self._stream()
+        self.lib.quantity(L, self.prec)
+        L.reserved0 = 0
+        return out
+
+    # ------------------------------------------------------------------ state
+    def state(self) -> torch.Tensor:
+        return self.fields_interior()
+
+    @property
+    def nodes(self) -> int:
+        return self.gshape[0] * self.gshape[1] * self.gshape[2]
+
+    def memory_bytes(self) -> int:
+        es = 4 if self.sdtype == torch.float32 else 8
+        return 2 * self.nf * self.fs * es + self.flags.numel() * self.flags.element_size()

@@ -1,0 +1,43 @@
+"""Model registry (replaces the reference's conf.mk discovery, src/models.R:20-90).
+
+Every model is a Python module exposing ``build() -> Model``; variants (the reference's
+``OPT=`` option products, e.g. ``d2q9_bc_autosym``) are registered as separate entries
+with option dictionaries."""
+from __future__ import annotations
+
+import importlib
+from typing import Callable, Dict, List, Optional
+
+from .dsl import Model
+
+# name -> (module, kwargs)
+_MODELS: Dict[str, tuple] = {}
+
+
+def register(name: str, module: str, **kwargs):
+    _MODELS[name] = (module, kwargs)
+
+
+def names() -> List[str]:
+    return sorted(_MODELS)
+
+
+_cache: Dict[str, Model] = {}
+
+
+def get(name: str) -> Model:
+    if name not in _MODELS:
+        raise KeyError(f"unknown model '{name}'; known: {', '.join(names())}")
+    if name not in _cache:
+        mod, kw = _MODELS[name]
+        m = importlib.import_module(mod, package=__package__)
+        model = m.build(**kw) if kw else m.build()
+        if model.name != name:
+            model.name = name
+        model.finalize()
+        _cache[name] = model
+    return _cache[name]
+
+
+# ---- catalog ---------------------------------------------------------------------
+register("d3q27", ".flow.d3q27")

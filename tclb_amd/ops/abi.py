@@ -1,0 +1,106 @@
+"""ctypes mirror of ``tclb::Launch`` (csrc/include/tclb/core.hpp) and the per-model
+kernel-library loader.
+
+The kernel libraries are plain C-ABI shared objects (no torch headers), loaded after
+``import torch`` so that they bind to the HIP runtime torch already loaded (both
+share the soname ``libamdhip64.so.7``).  On a GPU box a missing or failing HIP
+library is an error — there is no silent fallback to the CPU executor.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+from typing import Dict, Optional
+
+import torch  # noqa: F401  (must be imported before loading HIP libraries)
+
+
+class Launch(ctypes.Structure):
+    _fields_ = [
+        ("in_", ctypes.c_void_p),
+        ("out", ctypes.c_void_p),
+        ("flags", ctypes.c_void_p),
+        ("settings", ctypes.c_void_p),
+        ("zonal", ctypes.c_void_p),
+        ("globals_", ctypes.c_void_p),
+        ("aux", ctypes.c_void_p),
+        ("stream", ctypes.c_void_p),
+        ("sy", ctypes.c_longlong),
+        ("sz", ctypes.c_longlong),
+        ("fs", ctypes.c_longlong),
+        ("nx", ctypes.c_int), ("ny", ctypes.c_int), ("nz", ctypes.c_int), ("px", ctypes.c_int),
+        ("gy", ctypes.c_int), ("gz", ctypes.c_int),
+        ("x0", ctypes.c_int), ("y0", ctypes.c_int), ("z0", ctypes.c_int),
+        ("gnx", ctypes.c_int), ("gny", ctypes.c_int), ("gnz", ctypes.c_int),
+        ("xlo", ctypes.c_int), ("xhi", ctypes.c_int),
+        ("ylo", ctypes.c_int), ("yhi", ctypes.c_int),
+        ("zlo", ctypes.c_int), ("zhi", ctypes.c_int),
+        ("iter", ctypes.c_int),
+        ("nzones", ctypes.c_int),
+        ("stage", ctypes.c_int),
+        ("glob", ctypes.c_int),
+        ("quantity", ctypes.c_int),
+        ("qcomp", ctypes.c_int),
+        ("qscale", ctypes.c_double),
+        ("qsy", ctypes.c_longlong),
+        ("qsz", ctypes.c_longlong),
+        ("block_x", ctypes.c_int), ("block_y", ctypes.c_int),
+        ("reserved0", ctypes.c_int), ("reserved1", ctypes.c_int),
+    ]
+
+
+PREC = {"double": 0, "float": 1, "mixed": 2}
+
+
+class KernelError(RuntimeError):
+    pass
+
+
+class ModelLib:
+    """Handle on one compiled model library (HIP or CPU)."""
+
+    def __init__(self, model: str, kind: str, path: str):
+        self.model = model
+        self.kind = kind
+        self.path = path
+        self.lib = ctypes.CDLL(path, mode=ctypes.RTLD_LOCAL)
+        self._run = getattr(self.lib, f"tclb_{model}_run")
+        self._run.argtypes = [ctypes.POINTER(Launch), ctypes.c_int]
+        self._run.restype = ctypes.c_int
+        self._q = getattr(self.lib, f"tclb_{model}_quantity")
+        self._q.argtypes = [ctypes.POINTER(Launch), ctypes.c_int]
+        self._q.restype = ctypes.c_int
+        sz = getattr(self.lib, f"tclb_{model}_sizeof_launch")()
+        if sz != ctypes.sizeof(Launch):
+            raise KernelError(f"ABI mismatch for {path}: sizeof(Launch) {sz} != {ctypes.sizeof(Launch)}")
+
+    def run(self, L: Launch, prec: int):
+        r = self._run(ctypes.byref(L), prec)
+        if r != 0:
+            raise KernelError(f"{self.model}[{self.kind}] stage {L.stage} launch failed: code {r}")
+
+    def quantity(self, L: Launch, prec: int):
+        r = self._q(ctypes.byref(L), prec)
+        if r != 0:
+            raise KernelError(f"{self.model}[{self.kind}] quantity {L.quantity} failed: code {r}")
+
+
+_libs: Dict[tuple, ModelLib] = {}
+_lock = threading.Lock()
+
+
+def load(model: str, kind: str, build_if_missing: bool = True) -> ModelLib:
+    from .. import build as B
+    key = (model, kind)
+    with _lock:
+        if key in _libs:
+            return _libs[key]
+        path = B.lib_path(model, kind)
+        if build_if_missing and (not os.path.exists(path) or os.environ.get("TCLB_REBUILD")):
+            B.build_model(model, kinds=(kind,))
+        if not os.path.exists(path):
+            raise KernelError(f"kernel library for model '{model}' [{kind}] not built: {path}")
+        lib = ModelLib(model, kind, path)
+        _libs[key] = lib
+        return lib
