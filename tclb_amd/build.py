@@ -89,9 +89,31 @@ def build_model(name: str, kinds=("cpu", "hip"), force: bool = False, verbose: b
     return out
 
 
+def build_host(force: bool = False, verbose: bool = False) -> str:
+    """native host runtime library (geometry voxeliser, scans): libtclb_host.so"""
+    src = os.path.join(CSRC, "runtime", "host.cpp")
+    target = os.path.join(LIB, "libtclb_host.so")
+    os.makedirs(LIB, exist_ok=True)
+    cmd = [CXX, "-O3", "-std=c++17", "-fPIC", "-shared", "-fopenmp", src, "-o", target + ".tmp"]
+    h = _hash_inputs([src], " ".join(cmd))
+    stamp = target + ".hash"
+    if not force and os.path.exists(target) and os.path.exists(stamp) and open(stamp).read() == h:
+        return target
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"host library build failed:\n{r.stderr[-10000:]}")
+    os.replace(target + ".tmp", target)
+    with open(stamp, "w") as f:
+        f.write(h)
+    if verbose:
+        print("[tclb build] host runtime", flush=True)
+    return target
+
+
 def build_all(models: Optional[List[str]] = None, kinds=("cpu", "hip"), jobs: int = 0, force=False,
               verbose=False) -> Dict[str, Dict[str, str]]:
     models = models or registry.names()
+    build_host(force=force, verbose=verbose)
     jobs = jobs or max(1, min(8, os.cpu_count() or 1))
     tasks = [(m, k) for m in models for k in kinds]
     res: Dict[str, Dict[str, str]] = {m: {} for m in models}

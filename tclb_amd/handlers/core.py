@@ -1,0 +1,643 @@
+"""Core XML handlers (reference: src/Handlers/*.cpp, one class per element)."""
+from __future__ import annotations
+
+import collections
+import copy
+import math
+import os
+import xml.etree.ElementTree as ET
+from typing import List, Optional
+
+import numpy as np
+
+from ..utils.log import log
+from .base import (HANDLER_CALLBACK, ITERATION_STOP, Action, Callback, Design, GenericAction, GenericContainer,
+                   Handler, HandlerError, make_handler, register)
+
+
+def _what(node, default="all") -> List[str]:
+    return [w.strip() for w in node.get("what", default).split(",") if w.strip()]
+
+
+# ---------------------------------------------------------------------------- containers
+@register("CLBConfig")
+class MainContainer(GenericAction):
+    """reference MainContainer (src/Handlers/MainContainer.cpp:5-27)"""
+
+    def init(self):
+        super().init()
+        s = self.solver
+        fn = s.out_iter_file("config", ".xml")
+        if s.rank == 0:
+            cfg = copy.deepcopy(s.config_tree)
+            run = ET.SubElement(cfg, "Run", {"model": s.model_name})
+            ET.SubElement(run, "Code", {"version": "tclb_amd-0.1", "precision": s.precision,
+                                        "cross": "GPU" if s.lattice.is_gpu else "CPU"})
+            ET.ElementTree(cfg).write(fn)
+        return self.execute_internal()
+
+    def finish(self):
+        self.unstack()
+        return 0
+
+
+@register("Units", "Container")
+class UnitsContainer(GenericContainer):
+    """<Units> params are consumed before the run (reference readUnits); <Container> groups."""
+
+    def init(self):
+        if self.node.tag == "Units":
+            self.stack = 0
+            return 0
+        return super().init()
+
+
+@register("Model")
+class ModelContainer(GenericContainer):
+    """reference acModel: run children (Params), then lattice Init"""
+
+    def init(self):
+        r = super().init()
+        self.solver.lattice.init()
+        self.solver.iter = 0
+        return r
+
+
+@register("EvalIf")
+class IfContainer(GenericAction):
+    def init(self):
+        super().init()
+        present, missing = self.node.get("opt_present"), self.node.get("opt_missing")
+        if (present is None) == (missing is None):
+            raise HandlerError("Use either opt_present or opt_missing (not both) in EvalIf")
+        opt = present if present is not None else missing
+        opts = self.solver.model.options
+        if opt not in opts:
+            raise HandlerError(f"Unknown option in EvalIf: {opt}")
+        if bool(opts[opt]) == (present is not None):
+            return self.execute_internal()
+        return 0
+
+    def finish(self):
+        self.unstack()
+        return 0
+
+
+@register("Repeat")
+class Repeat(GenericAction):
+    def init(self):
+        super().init()
+        t = self.node.get("Times")
+        if t is None:
+            raise HandlerError("no Times parameter in Repeat")
+        for _ in range(int(t)):
+            self.execute_internal()
+            self.unstack()
+        return 0
+
+
+# ---------------------------------------------------------------------------- actions
+@register("Geometry")
+class GeometryAction(Action):
+    """reference acGeometry (src/Handlers/acGeometry.cpp:5-23)"""
+
+    def init(self):
+        super().init()
+        from ..geometry.geometry import Geometry
+        s = self.solver
+        lat = s.lattice
+        g = Geometry(s.model, lat.gshape, lat.slab.lo, lat.slab.n, lat.slab.axis, lat.g, units=s.units,
+                     permissive=s.permissive)
+        g.load(self.node)
+        s.geometry = g
+        lat.set_flags(g.flags)
+        for z in g.zones:
+            lat.add_zone(z)
+        if g.cuts is not None:
+            lat.set_cuts(g.cuts)
+        if self.node.get("save"):
+            g_path = self.node.get("save")
+            s.write_vtk("geometry", ["flag"], None) if g_path else None
+        return 0
+
+
+@register("Param")
+class Param(Action):
+    """reference acParam (src/Handlers/acParam.cpp:5-64)"""
+
+    def init(self):
+        super().init()
+        s = self.solver
+        par = self.node.get("name", "")
+        zone = self.node.get("zone", "")
+        value = self.node.get("value")
+        gauge = self.node.get("gauge")
+        permissive = str(self.context_attr("permissive", "false")).lower() in ("true", "1", "yes")
+        if zone and zone not in s.lattice.zone_names:
+            raise HandlerError(f"Unknown zone {zone} (found while setting parameter {par})")
+        if par == "":
+            if gauge is not None:
+                return 0
+            raise HandlerError("Setting name not specified in Param element")
+        st = s.model.setting(par)
+        if st is None:
+            if permissive:
+                log.warning(f"Unknown setting {par}")
+                return 0
+            raise HandlerError(f"Unknown setting {par}")
+        val = s.units.alt(value)
+        log.output(f"Setting {par}{' in zone ' + zone if zone else ''} to {value} ({val:g})")
+        s.lattice.set_setting(par, val, zone=zone or None)
+        return 0
+
+
+@register("Init")
+class InitAction(Action):
+    def init(self):
+        super().init()
+        self.solver.lattice.init()
+        self.solver.iter = 0
+        return 0
+
+
+@register("Solve")
+class Solve(GenericAction):
+    def init(self):
+        super().init()
+        self.execute_internal()
+        self.solve_loop()
+        self.unstack()
+        return 0
+
+
+@register("RunAction")
+class RunAction(GenericAction):
+    """reference acRunAction (src/Handlers/acRunAction.cpp:5-61)"""
+
+    def init(self):
+        super().init()
+        name = self.node.get("name", "")
+        if not name:
+            raise HandlerError("Have to specify the name of the Action in RunAction")
+        if self.solver.model.action(name) is None:
+            raise HandlerError(f"Unknown Action {name}")
+        self.execute_internal()
+        self.solve_loop(action=name)
+        self.unstack()
+        return 0
+
+
+@register("LoadBinary", "LoadMemoryDump")
+class LoadBinary(Action):
+    def init(self):
+        super().init()
+        f = self.node.get("file") or self.node.get("filename")
+        if f is None:
+            raise HandlerError("No file specified in LoadBinary")
+        self.solver.load_solution(f, comp=self.node.get("comp"))
+        return 0
+
+
+# ---------------------------------------------------------------------------- callbacks
+def _region_attrs(h, total):
+    x0, y0, z0, nx, ny, nz = total
+    reg = [x0, y0, z0, nx, ny, nz]
+    for i, a in enumerate("xyz"):
+        d = h.node.get("d" + a)
+        if d is not None:
+            v = int(round(h.solver.units.alt(d)))
+            if v < 0:
+                v = total[3 + i] + v
+            reg[i] = v
+            reg[3 + i] = total[3 + i] - v
+    for i, a in enumerate("xyz"):
+        n = h.node.get("n" + a)
+        if n is not None:
+            v = int(round(h.solver.units.alt(n)))
+            if v < 0:
+                v = total[3 + i] - reg[i] + v
+            reg[3 + i] = v
+    # intersect with total
+    for i in range(3):
+        lo = max(reg[i], total[i])
+        hi = min(reg[i] + reg[3 + i], total[i] + total[3 + i])
+        reg[i], reg[3 + i] = lo, max(0, hi - lo)
+    return tuple(reg)
+
+
+@register("VTK")
+class VTK(Callback):
+    """reference cbVTK (src/Handlers/cbVTK.cpp:5-68)"""
+
+    def init(self):
+        super().init()
+        self.name = self.node.get("name", "VTK")
+        self.what = _what(self.node)
+        self.reg = _region_attrs(self, self.solver.total)
+        if self.reg[3] * self.reg[4] * self.reg[5] == 0:
+            raise HandlerError(f'VTK "{self.name}" output has size 0')
+        return 0
+
+    def do_it(self):
+        return self.solver.write_vtk(self.name, self.what, self.reg)
+
+
+@register("TXT")
+class TXT(Callback):
+    def init(self):
+        super().init()
+        self.name = self.node.get("name", "TXT")
+        self.what = _what(self.node)
+        self.gzip = self.node.get("gzip", "false").lower() in ("true", "1")
+        return 0
+
+    def do_it(self):
+        return self.solver.write_txt(self.name, self.what, gzip=self.gzip)
+
+
+@register("BIN")
+class BIN(Callback):
+    def init(self):
+        super().init()
+        self.name = self.node.get("name", "BIN")
+        return 0
+
+    def do_it(self):
+        return self.solver.write_bin(self.name)
+
+
+@register("Log")
+class Log(Callback):
+    """reference cbLog: CSV log, forces ITER_LASTGLOB"""
+
+    def init(self):
+        super().init()
+        from ..solver import ITER_LASTGLOB
+        self.fn = self.solver.out_iter_file(self.node.get("name", "Log"), ".csv")
+        self.solver.init_log(self.fn)
+        self.old = self.solver.iter_type
+        self.solver.iter_type |= ITER_LASTGLOB
+        return 0
+
+    def do_it(self):
+        self.solver.write_log(self.fn)
+        return 0
+
+    def finish(self):
+        self.solver.iter_type = self.old
+        return 0
+
+
+@register("Failcheck")
+class Failcheck(Callback):
+    """reference cbFailcheck (src/Handlers/cbFailcheck.cpp:5-93): NaN scan, LOR, last words"""
+
+    def init(self):
+        super().init()
+        self.active = False
+        self.what = _what(self.node)
+        return 0
+
+    def do_it(self):
+        if self.active:
+            return 0
+        self.active = True
+        s = self.solver
+        fin = False
+        import torch
+        for q in s.model.quantities:
+            if "all" in self.what or q.name in self.what:
+                a = s.lattice.quantity(q.name)
+                bad = 0.0 if bool(torch.isfinite(a).all().item()) else 1.0
+                if s.comm.allreduce_scalar(bad, "max") > 0:
+                    log.notice(f"Checking {q.name} discovered NaN")
+                    fin = True
+                    break
+        self.active = False
+        if fin:
+            log.notice("NaN value discovered. Executing final actions from the Failcheck element before full stop...")
+            for c in list(self.node):
+                h = make_handler(c, s)
+                if h is not None:
+                    h.do_it()
+            log.notice("Stopping due to Nan value")
+            return ITERATION_STOP
+        return 0
+
+
+@register("Stop")
+class Stop(Callback):
+    """reference cbStop (src/Handlers/cbStop.cpp:12-106)"""
+
+    def init(self):
+        super().init()
+        from ..solver import ITER_LASTGLOB
+        self.checks = []
+        for g in self.solver.model.globals_:
+            for kind in ("Change", "PercentChange", "Above", "Below"):
+                v = self.node.get(g.name + kind)
+                if v is not None:
+                    self.checks.append([g.name, kind, float(v), -12341234.0])
+        if not self.checks:
+            raise HandlerError(f"No *Change attribute in {self.node.tag}")
+        self.times = int(self.node.get("Times", "1"))
+        if self.times < 1:
+            raise HandlerError("Minimal number for Times attribute is 1")
+        self.score = 0
+        self.old = self.solver.iter_type
+        self.solver.iter_type |= ITER_LASTGLOB
+        return 0
+
+    def do_it(self):
+        g = self.solver.lattice.globals
+        anyc = 0
+        for c in self.checks:
+            name, kind, lim, old = c
+            v = g.get(name, 0.0)
+            if kind == "Change" and abs(old - v) > lim:
+                anyc += 1
+            elif kind == "PercentChange" and (v == 0 or abs((old - v) / v) > lim):
+                anyc += 1
+            elif kind == "Above" and v < lim:
+                anyc += 1
+            elif kind == "Below" and v > lim:
+                anyc += 1
+            c[3] = v
+        self.score = self.score + 1 if anyc == 0 else 0
+        log.output(f"Stop criterium score: {self.score}")
+        if self.score >= self.times:
+            log.notice("Stop.")
+            for c in self.checks:
+                c[3] = -12341234.0
+            self.score = 0
+            return ITERATION_STOP
+        return 0
+
+    def finish(self):
+        self.solver.iter_type = self.old
+        return 0
+
+
+@register("SaveCheckpoint")
+class SaveCheckpoint(Callback):
+    """reference cbSaveCheckpoint (src/Handlers/cbSaveCheckpoint.cpp:5-107)"""
+
+    def init(self):
+        super().init()
+        k = self.node.get("keep")
+        if k is None:
+            self.keep = 1
+        elif k == "all":
+            self.keep = 0
+        else:
+            self.keep = int(k)
+            if self.keep < 0:
+                self.keep = 1
+        self.q = collections.deque()
+        return 0
+
+    def do_it(self):
+        s = self.solver
+        fn = s.out_iter_collective_file("checkpoint", "")
+        rf = s.out_iter_collective_file("restart", ".xml")
+        path = s.save_solution(fn)
+        if s.rank == 0:
+            self.write_restart(path, rf)
+        if self.keep:
+            self.q.append((path, rf))
+            while len(self.q) > self.keep:
+                p, r = self.q.popleft()
+                if s.rank == 0:
+                    for f in (p, p + ".json", r):
+                        if os.path.exists(f):
+                            os.remove(f)
+        return 0
+
+    def write_restart(self, path, rf):
+        cfg = copy.deepcopy(self.solver.config_tree)
+        lb = cfg.find("LoadBinary")
+        if lb is None:
+            solve = cfg.find("Solve")
+            idx = list(cfg).index(solve) if solve is not None else len(cfg)
+            lb = ET.Element("LoadBinary", {"file": path})
+            cfg.insert(idx, lb)
+        else:
+            lb.set("file", path)
+        ET.ElementTree(cfg).write(rf)
+
+
+@register("SaveBinary", "SaveMemoryDump")
+class SaveBinary(Callback):
+    def init(self):
+        super().init()
+        self.name = self.node.get("filename") or self.node.get("file") or "Save"
+        return 0
+
+    def do_it(self):
+        s = self.solver
+        if self.node.get("filename") or self.node.get("file"):
+            path = self.name
+        else:
+            path = s.out_iter_collective_file(self.name, "")
+        s.save_solution(path)
+        return 0
+
+
+@register("Average")
+class Average(Callback):
+    """reference cbAveraging: reset averaged densities"""
+
+    def do_it(self):
+        self.solver.lattice.reset_average()
+        return 0
+
+
+@register("DumpSettings")
+class DumpSettings(Callback):
+    def do_it(self):
+        s = self.solver
+        if s.rank == 0:
+            fn = s.out_iter_file(self.node.get("name", "Settings"), ".csv")
+            with open(fn, "w") as f:
+                f.write("setting,zone,value\n")
+                for st in s.model.settings:
+                    if st.zonal:
+                        for z in s.lattice.zone_names:
+                            f.write(f"{st.name},{z},{s.lattice.get_setting(st.name, z):.13e}\n")
+                    else:
+                        f.write(f"{st.name},,{s.lattice.get_setting(st.name):.13e}\n")
+        return 0
+
+
+@register("Sample")
+class Sample(Callback):
+    """reference cbSample + Sampler (src/Handlers/cbSample.cpp:5-60, src/Sampler.cpp:16-99):
+    probe points, quantities appended to a CSV on the owning rank"""
+
+    def init(self):
+        super().init()
+        s = self.solver
+        self.what = _what(self.node)
+        self.points = []
+        for p in self.node.findall("Point"):
+            x = int(round(s.units.alt(p.get("dx", "0"))))
+            y = int(round(s.units.alt(p.get("dy", "0"))))
+            z = int(round(s.units.alt(p.get("dz", "0"))))
+            self.points.append((x, y, z))
+        self.fn = s.out_iter_file(self.node.get("name", "Sampler"), ".csv")
+        self.qs = [q for q in s.model.quantities if "all" in self.what or q.name in self.what]
+        lat = s.lattice
+        ox, oy, oz = lat.slab.offset
+        nx, ny, nz = lat.shape
+        self.mine = [(i, p) for i, p in enumerate(self.points)
+                     if oy <= p[1] < oy + ny and oz <= p[2] < oz + nz and 0 <= p[0] < nx]
+        if self.mine:
+            with open(self.fn, "w") as f:
+                cols = ["Iteration", "point", "x", "y", "z"]
+                for q in self.qs:
+                    cols += [q.name + c for c in (".x", ".y", ".z")] if q.vector else [q.name]
+                f.write(",".join(cols) + "\n")
+        return 0
+
+    def do_it(self):
+        if not self.mine:
+            return 0
+        s = self.solver
+        lat = s.lattice
+        ox, oy, oz = lat.slab.offset
+        vals = {q.name: s.quantity_si(q.name) for q in self.qs}
+        with open(self.fn, "a") as f:
+            for i, (x, y, z) in self.mine:
+                row = [str(s.iter), str(i), str(x), str(y), str(z)]
+                for q in self.qs:
+                    a = vals[q.name][:, z - oz, y - oy, x]
+                    row += [f"{v:.13e}" for v in a]
+                f.write(",".join(row) + "\n")
+        return 0
+
+
+@register("PID")
+class PID(Callback):
+    """reference cbPID (src/Handlers/cbPID.cpp:94-122): drive a (zonal) setting so that a
+    global reaches a target."""
+
+    def init(self):
+        super().init()
+        n = self.node
+        s = self.solver
+        self.control = n.get("control")
+        self.zone = n.get("zone")
+        self.what = None
+        self.target = None
+        for g in s.model.globals_:
+            if n.get(g.name) is not None:
+                self.what = g.name
+                self.target = s.units.alt(n.get(g.name))
+        if self.what is None or self.control is None:
+            raise HandlerError("PID needs a <Global>=target attribute and control=")
+        self.P = float(n.get("P", "1"))
+        self.I = float(n.get("I", "0"))
+        self.D = float(n.get("D", "0"))
+        self.DT = float(n.get("DerivativeTime", n.get("DT", "0")))
+        self.integral = 0.0
+        self.prev = None
+        from ..solver import ITER_LASTGLOB
+        s.iter_type |= ITER_LASTGLOB
+        return 0
+
+    def do_it(self):
+        s = self.solver
+        v = s.lattice.globals.get(self.what, 0.0)
+        err = self.target - v
+        self.integral += err * self.every_iter
+        der = 0.0 if self.prev is None else (err - self.prev) / max(self.every_iter, 1)
+        self.prev = err
+        u = self.P * (err + self.I * self.integral + self.D * der)
+        s.lattice.set_setting(self.control, u, zone=self.zone)
+        return 0
+
+
+@register("Keep")
+class Keep(Callback):
+    """reference cbKeep (src/Handlers/cbKeep.cpp:45-66): objective constraint weight"""
+
+    def init(self):
+        super().init()
+        n = self.node
+        s = self.solver
+        self.items = []
+        for g in s.model.globals_:
+            for kind in ("Above", "Below", "Equal"):
+                v = n.get(g.name + kind)
+                if v is not None:
+                    self.items.append((g.name, kind, s.units.alt(v)))
+        self.force = float(n.get("Force", "1"))
+        return 0
+
+    def do_it(self):
+        s = self.solver
+        for name, kind, thr in self.items:
+            v = s.lattice.globals.get(name, 0.0)
+            w = self.force * (thr - v)
+            if kind == "Above" and v > thr:
+                w = 0.0
+            if kind == "Below" and v < thr:
+                w = 0.0
+            s.lattice.set_setting(name + "InObj", w)
+        return 0
+
+
+@register("RunPython")
+class RunPython(Callback):
+    """Embedded Python callback (reference RunR/RunPython, src/Handlers/cbRunR.cpp:687-845).
+    The element text is executed with ``solver``, ``lattice``, ``np``, ``torch`` in scope."""
+
+    def init(self):
+        super().init()
+        self.code = (self.node.text or "").strip()
+        if self.every_iter == 0:
+            pass
+        return 0
+
+    def do_it(self):
+        import torch
+        s = self.solver
+        env = {"solver": s, "lattice": s.lattice, "np": np, "torch": torch, "iteration": s.iter}
+        exec(compile(self.code, "<RunPython>", "exec"), env)
+        return 0
+
+
+@register("Control")
+class Control(GenericAction):
+    """reference conControl (src/Handlers/conControl.cpp:108-257): time-dependent settings.
+    Supported: <CSV file= Time=> column interpolation and <Param name= value=> with
+    ``Iterations`` period; values interpolated linearly every iteration segment."""
+
+    kind = HANDLER_CALLBACK
+
+    def init(self):
+        super().init()
+        s = self.solver
+        self.series = []  # (setting, zone, times(array), values(array))
+        for c in self.node:
+            if c.tag == "CSV":
+                import csv
+                with open(c.get("file")) as f:
+                    rows = list(csv.DictReader(f))
+                tcol = c.get("Time", "Time")
+                t = np.array([s.units.alt(r[tcol]) for r in rows])
+                for col in rows[0]:
+                    if col == tcol:
+                        continue
+                    if s.model.setting(col) is not None:
+                        self.series.append((col, None, t, np.array([s.units.alt(r[col]) for r in rows])))
+            elif c.tag == "Param":
+                pass
+        self.every_iter = 1.0
+        return 0
+
+    def do_it(self):
+        s = self.solver
+        for name, zone, t, v in self.series:
+            s.lattice.set_setting(name, float(np.interp(s.iter, t, v)), zone=zone)
+        return 0

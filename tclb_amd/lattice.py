@@ -349,6 +349,20 @@ class Lattice:
         nx, ny, nz = self.shape
         return a[self.gz:self.gz + nz, self.gy:self.gy + ny, :nx]
 
+    def set_cuts(self, cuts: np.ndarray):
+        """sub-voxel cuts (26, NZ, NY, nx) uint16 for interpolated bounce-back models"""
+        nx = self.shape[0]
+        full = np.full((26, self.NZ, self.NY, self.px), 65535, dtype=np.uint16)
+        full[:, :, :, :nx] = cuts
+        self.cuts = torch.from_numpy(full.view(np.int16)).to(self.device)
+
+    def reset_average(self):
+        """reset averaged fields (reference cbAveraging -> resetAverage, src/Lattice.cu.Rt:1360-1365)"""
+        idx = [i for i, f in enumerate(self.model.fields) if f.average]
+        for i in idx:
+            self.snaps[self.cur][i].zero_()
+        self.average_start = self.iter
+
     # ------------------------------------------------------------------ fields / quantities
     def field(self, name: str) -> torch.Tensor:
         """interior view of a stored field in the current snapshot: (nz, ny, nx)"""

@@ -1,0 +1,68 @@
+"""d2q9 — weighted-orthogonal MRT with Zou/He (rewrite form) velocity/pressure
+boundaries, symmetry and bounce-back; objective globals on Inlet/Outlet nodes.
+Reference: models/flow/d2q9/Dynamics.R, Dynamics.c.Rt (base variant, no bc/autosym)."""
+import numpy as np
+import sympy as sp
+
+from ..dsl import Model
+from ...emit.symbolic import mrt_eq, poly_matrix, weights_from_eq
+from ...emit.blocks import mrt_block
+
+U9 = np.array([[0, 0], [1, 0], [0, 1], [-1, 0], [0, -1], [1, 1], [-1, 1], [-1, -1], [1, -1]])
+
+
+def d2q9_mrt_basis():
+    """B = M H^T with H from the Cholesky factor of M^-1 diag(1/w) M^-T (reversed order),
+    rows scaled by (1, sqrt3/3, sqrt3/3, sqrt2, sqrt2, 1, sqrt6/3, sqrt6/3, 2)
+    (reference models/flow/d2q9/Dynamics.c.Rt:8-24)."""
+    raw = mrt_eq(U9, orthogonal=False)
+    M = raw.mat
+    w = weights_from_eq(raw)
+    Minv = M.inv()
+    W = Minv * sp.diag(*[1 / x for x in w]) * Minv.T
+    n = W.shape[0]
+    rev = list(range(n))[::-1]
+    Wr = W.extract(rev, rev)
+    L = Wr.cholesky(hermitian=False)   # Wr = L L^T
+    Ur = L.T                           # R's chol(): upper factor
+    H = Ur.extract(rev, rev)
+    scale = [1, sp.sqrt(3) / 3, sp.sqrt(3) / 3, sp.sqrt(2), sp.sqrt(2), 1, sp.sqrt(6) / 3, sp.sqrt(6) / 3, 2]
+    H = sp.Matrix(n, n, lambda r, c: sp.nsimplify(sp.simplify(H[r, c] * scale[r])))
+    B = (M * H.T).applyfunc(sp.simplify)
+    return B
+
+
+def build(bc: bool = False) -> Model:
+    m = Model("d2q9", dims=2, family="flow", reference="models/flow/d2q9",
+              description="D2Q9 MRT (weighted orthogonal basis) with Zou/He and symmetry boundaries")
+    shifts = [4 / 9] + [1 / 9] * 4 + [1 / 36] * 4
+    for i, (x, y) in enumerate(U9):
+        m.add_density(f"f[{i}]", int(x), int(y), 0, group="f", shift=shifts[i])
+    m.add_quantity("Rho", unit="kg/m3")
+    m.add_quantity("U", unit="m/s", vector=True)
+    m.add_setting("RelaxationRate", comment="one over relaxation time", S2="1-RelaxationRate")
+    m.add_setting("Viscosity", default=0.16666666, comment="viscosity", RelaxationRate="1.0/(3*Viscosity + 0.5)")
+    m.add_setting("VelocityX", default=0, comment="inlet/outlet/init velocity", zonal=True, unit="m/s")
+    m.add_setting("VelocityY", default=0, comment="inlet/outlet/init velocity", zonal=True, unit="m/s")
+    m.add_setting("Pressure", default=0, comment="inlet/outlet/init density", zonal=True, unit="Pa")
+    m.add_setting("GravitationX")
+    m.add_setting("GravitationY")
+    m.add_global("PressureLoss", comment="pressure loss", unit="1mPa")
+    m.add_global("OutletFlux", comment="pressure loss", unit="1m2/s")
+    m.add_global("InletFlux", comment="pressure loss", unit="1m2/s")
+    m.add_setting("S2", default=0, comment="MRT Sx")
+    m.add_setting("S3", default=0, comment="MRT Sx")
+    m.add_setting("S4", default=0, comment="MRT Sx")
+    for n in ["EPressure", "WPressure", "NVelocity", "SVelocity", "WVelocity", "EVelocity", "NSymmetry", "SSymmetry"]:
+        m.add_node_type(n, "BOUNDARY")
+    m.add_node_type("Inlet", "OBJECTIVE")
+    m.add_node_type("Outlet", "OBJECTIVE")
+    m.add_node_type("Solid", "BOUNDARY")
+    m.add_node_type("Wall", "BOUNDARY")
+    m.add_node_type("MRT", "COLLISION")
+    m.options = {"bc": bc, "autosym": False}
+    B = d2q9_mrt_basis()
+    eq = mrt_eq(U9, mat=B)
+    m.add_codegen(lambda _m: mrt_block("mrt", eq))
+    m.set_dynamics("flow/d2q9.inc")
+    return m

@@ -41,3 +41,4 @@ def get(name: str) -> Model:
 
 # ---- catalog ---------------------------------------------------------------------
 register("d3q27", ".flow.d3q27")
+register("d2q9", ".flow.d2q9")

@@ -1,0 +1,62 @@
+"""ctypes bindings of the native host runtime library (libtclb_host.so)."""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import numpy as np
+
+_lib = None
+_lock = threading.Lock()
+
+
+def lib():
+    global _lib
+    with _lock:
+        if _lib is None:
+            from .. import build as B
+            path = os.path.join(B.LIB, "libtclb_host.so")
+            if not os.path.exists(path):
+                B.build_host()
+            L = ctypes.CDLL(path)
+            P = ctypes.c_void_p
+            i = ctypes.c_int
+            L.tclb_stl_fill.argtypes = [P, i, i, i, i, i, i, i, i, P]
+            L.tclb_stl_fill.restype = ctypes.c_longlong
+            L.tclb_stl_cuts.argtypes = [P, i, i, i, i, i, i, i, P, P, P]
+            L.tclb_stl_cuts.restype = ctypes.c_longlong
+            L.tclb_nan_scan_f64.argtypes = [P, ctypes.c_longlong]
+            L.tclb_nan_scan_f64.restype = ctypes.c_longlong
+            L.tclb_nan_scan_f32.argtypes = [P, ctypes.c_longlong]
+            L.tclb_nan_scan_f32.restype = ctypes.c_longlong
+            _lib = L
+    return _lib
+
+
+def stl_fill(tri: np.ndarray, region, axis: int, inside_out: int) -> np.ndarray:
+    x0, y0, z0, nx, ny, nz = region
+    lev = np.full((nz, ny, nx), inside_out, dtype=np.uint8)
+    t = np.ascontiguousarray(tri, dtype=np.float64)
+    lib().tclb_stl_fill(t.ctypes.data, len(t), x0, y0, z0, nx, ny, nz, axis, lev.ctypes.data)
+    return lev
+
+
+def stl_cuts(tri: np.ndarray, region, dirs: np.ndarray):
+    x0, y0, z0, nx, ny, nz = region
+    cuts = np.full((26, nz, ny, nx), 65535, dtype=np.uint16)
+    mask = np.zeros((nz, ny, nx), dtype=np.uint8)
+    t = np.ascontiguousarray(tri, dtype=np.float64)
+    d = np.ascontiguousarray(dirs, dtype=np.int32)
+    lib().tclb_stl_cuts(t.ctypes.data, len(t), x0, y0, z0, nx, ny, nz, d.ctypes.data, cuts.ctypes.data,
+                        mask.ctypes.data)
+    return cuts, mask
+
+
+def nan_count(a: np.ndarray) -> int:
+    a = np.ascontiguousarray(a)
+    if a.dtype == np.float64:
+        return int(lib().tclb_nan_scan_f64(a.ctypes.data, a.size))
+    if a.dtype == np.float32:
+        return int(lib().tclb_nan_scan_f32(a.ctypes.data, a.size))
+    return int((~np.isfinite(a)).sum())

@@ -1,0 +1,287 @@
+"""Solver facade: case set-up, output naming, logs, handler stack.
+
+Re-design of the reference's Solver + main() (reference: src/Solver.h.Rt:60-187,
+src/Solver.cpp.Rt, src/main.cpp:173-425).  The whole run happens inside the root
+handler's init (CLBConfig), exactly as in the reference (src/main.cpp:404-410).
+"""
+from __future__ import annotations
+
+import copy
+import json
+import os
+import time
+import xml.etree.ElementTree as ET
+from typing import Dict, List, Optional, Sequence
+
+import numpy as np
+import torch
+
+from .geometry.geometry import Geometry
+from .lattice import Lattice
+from .models import registry
+from .parallel.comm import Comm, LoopbackComm, init_distributed_from_env
+from .utils.log import log
+from .utils.units import UnitEnv, UnitVal
+
+ITER_NORM = 0x00
+ITER_GLOBS = 0x01
+ITER_LASTGLOB = 0x02
+ITERATION_STOP = 1
+
+
+class SolverError(RuntimeError):
+    pass
+
+
+class Solver:
+    def __init__(self, model: str, config: ET.Element, conffile: str = "case.xml", device: Optional[str] = None,
+                 precision: str = "double", comm: Optional[Comm] = None, block=(0, 0)):
+        self.model_name = model
+        self.model = registry.get(model)
+        self.config_tree = config
+        self.conffile = conffile
+        self.comm = comm or LoopbackComm()
+        self.rank = self.comm.rank
+        self.size = self.comm.size
+        self.precision = precision
+        self.block = block
+        if device is None:
+            device = "cuda" if torch.cuda.is_available() else "cpu"
+        if device == "cuda":
+            local = int(os.environ.get("LOCAL_RANK", "0"))
+            self.device = torch.device("cuda", local % max(1, torch.cuda.device_count()))
+        else:
+            self.device = torch.device(device)
+        self.units = UnitEnv()
+        self.iter = 0
+        self.steps = 1
+        self.iter_type = ITER_NORM
+        self.opt_iter = 0
+        self.hands: List = []
+        self.lattice: Optional[Lattice] = None
+        self.geometry: Optional[Geometry] = None
+        self.outpath = ""
+        self.permissive = (config.get("permissive", "false").lower() in ("true", "1", "yes"))
+        self.start_time = time.time()
+        self.log_scales: Dict[str, float] = {}
+        self.set_output(config.get("output", ""))
+        self._meter_t = time.time()
+        self._meter_it = 0
+
+    # ------------------------------------------------------------------ setup
+    def read_units(self):
+        """reference readUnits (src/main.cpp:31-63) + Solver::setUnit (src/Solver.cpp.Rt:90-103)"""
+        u = self.config_tree.find("Units")
+        if u is None:
+            return
+        for i, p in enumerate(u.findall("Param")):
+            if p.get("value") is None or p.get("gauge") is None:
+                raise SolverError("Units Param needs value and gauge")
+            name = p.get("name", f"unnamed{i + 1}")
+            self.units.set_unit(name, self.units.read_text(p.get("value")) / self.units.read_text(p.get("gauge")), 1.0)
+        self.units.make_gauge()
+
+    def set_size(self):
+        g = self.config_tree.find("Geometry")
+        if g is None:
+            raise SolverError("no Geometry element")
+        nx = int(round(self.units.alt(g.get("nx", "1"), 1)))
+        ny = int(round(self.units.alt(g.get("ny", "1"), 1)))
+        nz = int(round(self.units.alt(g.get("nz", "1"), 1)))
+        log.notice(f"Mesh size in config file: {nx}x{ny}x{nz}")
+        self.lattice = Lattice(self.model, (nx, ny, nz), device=self.device, precision=self.precision,
+                               comm=self.comm, block=self.block)
+        self.total = (0, 0, 0, nx, ny, nz)
+
+    def set_output(self, out: str):
+        base = os.path.splitext(os.path.basename(self.conffile))[0]
+        self.outpath = f"{out}{base}"
+
+    def out_iter_file(self, name: str, suffix: str) -> str:
+        p = f"{self.outpath}_{name}_P{self.rank:02d}_{self.iter:08d}{suffix}"
+        os.makedirs(os.path.dirname(p) or ".", exist_ok=True)
+        return p
+
+    def out_global_file(self, name: str, suffix: str) -> str:
+        p = f"{self.outpath}_{name}_P{self.rank:02d}{suffix}"
+        os.makedirs(os.path.dirname(p) or ".", exist_ok=True)
+        return p
+
+    def out_iter_collective_file(self, name: str, suffix: str) -> str:
+        p = f"{self.outpath}_{name}_{self.iter:08d}{suffix}"
+        os.makedirs(os.path.dirname(p) or ".", exist_ok=True)
+        return p
+
+    # ------------------------------------------------------------------ running
+    def run(self):
+        from .handlers.base import make_handler
+        self.read_units()
+        self.set_size()
+        root = make_handler(self.config_tree, self)
+        if root is None:
+            raise SolverError("root handler failed")
+        root.finish()
+        return 0
+
+    def iterate(self, steps: int, action: Optional[str] = None):
+        """one Solve segment (reference Lattice::Iterate with iter_type)"""
+        lat = self.lattice
+        glob = bool(self.iter_type & (ITER_LASTGLOB | ITER_GLOBS))
+        if action is None:
+            lat.iterate(steps, glob_last=glob)
+        else:
+            lat.iterate(steps, glob_last=glob, action=action)
+        self.iter += steps
+        self._speed_meter(steps)
+
+    def _speed_meter(self, steps: int):
+        """reference MainCallback (src/main.cpp:68-157): MLBUps / GB/s"""
+        self._meter_it += steps
+        now = time.time()
+        dt = now - self._meter_t
+        if dt > 1.0:
+            if self.lattice.is_gpu:
+                torch.cuda.synchronize()
+                now = time.time()
+                dt = now - self._meter_t
+            mlups = self.lattice.nodes * self._meter_it / dt / 1e6
+            es = 4 if self.lattice.sdtype == torch.float32 else 8
+            gbs = mlups * (2 * self.lattice.nf * es + self.lattice.flags.element_size()) / 1e3
+            log.output(f"{self.iter:8d} it {mlups:8.1f} MLBUps {gbs:7.2f} GB/s")
+            self._meter_t = now
+            self._meter_it = 0
+
+    # ------------------------------------------------------------------ outputs
+    def quantity_si(self, name: str) -> np.ndarray:
+        q = next(q for q in self.model.quantities if q.name == name)
+        v = self.units.unit_scale(q.unit)
+        return self.lattice.quantity(name, scale=1.0 / v).cpu().numpy()
+
+    def write_vtk(self, name: str, what: Optional[Sequence[str]], region=None):
+        from .io import vtk
+        lat = self.lattice
+        fn = self.out_iter_file(name, ".vti")
+        log.output(f"{self.iter:8d} it writing vtk {fn}")
+        allq = what is None or "all" in what
+        fields = []
+        flags = lat.get_flags()
+        if what is not None and "flag" in what:
+            fields.append(("flag", flags.astype(np.uint16 if self.model.flag_bits == 16 else np.uint32), 1))
+        for gname in sorted(self.model.group_masks):
+            if gname in ("ALL", "NONE"):
+                continue
+            if (allq and gname != "SETTINGZONE" and gname in {n.group for n in self.model.node_types}) or \
+                    (what is not None and gname in what):
+                mask = self.model.group_masks[gname]
+                shift = self.model.group_shift.get(gname, 0)
+                fields.append((gname, ((flags & mask) >> shift).astype(np.uint8), 1))
+        for q in self.model.quantities:
+            if allq or (what is not None and q.name in what):
+                a = self.quantity_si(q.name)
+                if q.vector:
+                    fields.append((q.name, a, 3))
+                else:
+                    fields.append((q.name, a[0], 1))
+        sx, sy, sz = lat.slab.offset
+        nx, ny, nz = lat.shape
+        reg = (sx, sy, sz, nx, ny, nz)
+        region = region or self.total
+        sub = _crop(fields, reg, region)
+        spacing = 1.0 / self.units.alt("1m") if self.units.alt("1m") != 0 else 1.0
+        if sub is not None:
+            lreg, lfields = sub
+            vtk.write_vti(fn, region, lreg, lfields, spacing=spacing)
+        regs = self.comm.gather_objects(sub[0] if sub is not None else None)
+        names = self.comm.gather_objects(os.path.basename(fn) if sub is not None else None)
+        if self.rank == 0:
+            pieces = [(r, n) for r, n in zip(regs, names) if r is not None]
+            meta = [(nme, vtk._VTK_T[np.asarray(a).dtype], nc) for nme, a, nc in fields]
+            vtk.write_pvti(fn[:-4] + ".pvti", region, pieces, meta, spacing=spacing)
+        return 0
+
+    def write_txt(self, name: str, what: Optional[Sequence[str]], gzip: bool = False):
+        prefix = self.out_iter_file(name, "")
+        for q in self.model.quantities:
+            if what is None or "all" in what or q.name in what:
+                a = self.quantity_si(q.name)
+                fn = f"{prefix}_{q.name}.txt"
+                arr = a.reshape(a.shape[0], -1).T
+                if gzip:
+                    import gzip as gz
+                    with gz.open(fn + ".gz", "wt") as f:
+                        np.savetxt(f, arr)
+                else:
+                    np.savetxt(fn, arr)
+        return 0
+
+    def write_bin(self, name: str):
+        """raw dump of every stored field (reference binWriteLattice, src/vtkLattice.cpp:56-80)"""
+        prefix = self.out_iter_file(name, "")
+        f = self.lattice.fields_interior().cpu().numpy()
+        for i, fl in enumerate(self.model.fields):
+            f[i].tofile(f"{prefix}_{fl.nicename}.bin")
+        return 0
+
+    # ---- CSV log (reference Solver::initLog/writeLog, src/Solver.cpp.Rt:120-206)
+    def _log_columns(self):
+        lat = self.lattice
+        cols = []
+        for s in self.model.global_settings:
+            cols.append((s.name, lambda s=s: lat.get_setting(s.name), s.unit))
+        for s in self.model.zonal_settings:
+            for z in sorted(lat.zone_names):
+                cols.append((f"{s.name}-{z}", lambda s=s, z=z: lat.get_setting(s.name, z), s.unit))
+        for g in self.model.globals_:
+            cols.append((g.name, lambda g=g: lat.globals.get(g.name, 0.0), g.unit))
+        return cols
+
+    def init_log(self, fn: str):
+        if self.rank != 0:
+            return
+        cols = self._log_columns()
+        hdr = ['"Iteration"', '"Time_si"', '"Walltime"', '"Optimization"']
+        for n, _, _ in cols:
+            hdr += [f'"{n}"', f'"{n}_si"']
+        hdr += ['"dx_si"', '"dt_si"', '"dm_si"']
+        with open(fn, "w") as f:
+            f.write(",".join(hdr) + "\n")
+
+    def write_log(self, fn: str):
+        if self.rank != 0:
+            return
+        dt = 1.0 / self.units.alt("1s")
+        row = [f"{self.iter}", f"{dt * self.iter:.13e}", f"{time.time() - self.start_time:.13e}", f"{self.opt_iter}"]
+        for n, get, unit in self._log_columns():
+            v = get()
+            sc = 1.0 / self.units.unit_scale(unit)
+            row += [f"{v:.13e}", f"{v * sc:.13e}"]
+        row += [f"{1.0 / self.units.alt('1m'):.13e}", f"{dt:.13e}", f"{1.0 / self.units.alt('1kg'):.13e}"]
+        with open(fn, "a") as f:
+            f.write(", ".join(row) + "\n")
+
+    # ---- checkpoints (portable: global-index layout, any rank count)
+    def save_solution(self, prefix: str) -> str:
+        from .io.checkpoint import save_state
+        return save_state(self, prefix)
+
+    def load_solution(self, path: str, comp: Optional[str] = None):
+        from .io.checkpoint import load_state
+        load_state(self, path, comp=comp)
+
+
+def _crop(fields, reg, region):
+    """crop local arrays (covering reg) to the output region; returns (lreg, fields)"""
+    x0, y0, z0, nx, ny, nz = reg
+    X0, Y0, Z0, NX, NY, NZ = region
+    a0, a1 = max(x0, X0), min(x0 + nx, X0 + NX)
+    b0, b1 = max(y0, Y0), min(y0 + ny, Y0 + NY)
+    c0, c1 = max(z0, Z0), min(z0 + nz, Z0 + NZ)
+    if a1 <= a0 or b1 <= b0 or c1 <= c0:
+        return None
+    out = []
+    for name, a, nc in fields:
+        if nc > 1:
+            out.append((name, a[:, c0 - z0:c1 - z0, b0 - y0:b1 - y0, a0 - x0:a1 - x0], nc))
+        else:
+            out.append((name, a[c0 - z0:c1 - z0, b0 - y0:b1 - y0, a0 - x0:a1 - x0], nc))
+    return (a0, b0, c0, a1 - a0, b1 - b0, c1 - c0), out

@@ -1,0 +1,99 @@
+import os
+import shutil
+import subprocess
+import sys
+import xml.etree.ElementTree as ET
+
+import numpy as np
+import pytest
+
+from tclb_amd import handlers  # noqa: F401
+from tclb_amd.io.vtk import read_vti
+from tclb_amd.solver import Solver
+from tclb_amd.utils.xpath import apply_edits
+
+KARMAN = """<?xml version="1.0"?>
+<CLBConfig version="2.0" output="output/" permissive="true">
+  <Geometry nx="128" ny="32">
+    <MRT><Box/></MRT>
+    <WVelocity name="Inlet"><Inlet/></WVelocity>
+    <EPressure name="Outlet"><Outlet/></EPressure>
+    <Inlet nx="1" dx="5"><Box/></Inlet>
+    <Outlet nx="1" dx="-5"><Box/></Outlet>
+    <Wall mask="ALL"><Channel/><Wedge dx="30" nx="8" dy="12" ny="8" direction="LowerRight"/></Wall>
+  </Geometry>
+  <Model>
+    <Param name="VelocityX" value="0.02"/>
+    <Param name="Viscosity" value="0.05"/>
+    <Param name="Smag" value="0.16"/>
+  </Model>
+  <VTK Iterations="50"/>
+  <Log Iterations="25"/>
+  <Failcheck Iterations="50"/>
+  <Solve Iterations="100"/>
+</CLBConfig>"""
+
+
+def run_case(tmp_path, xml, model="d2q9", edits=()):
+    os.chdir(tmp_path)
+    root = ET.fromstring(xml)
+    root, _ = apply_edits(root, list(edits))
+    s = Solver(model, root, conffile=str(tmp_path / "case.xml"), device="cpu")
+    s.run()
+    return s
+
+
+def test_karman_run(tmp_path):
+    s = run_case(tmp_path, KARMAN)
+    assert s.iter == 100
+    out = sorted(os.listdir(tmp_path / "output"))
+    assert "case_VTK_P00_00000050.vti" in out and "case_VTK_P00_00000100.pvti" in out
+    d = read_vti(str(tmp_path / "output" / "case_VTK_P00_00000100.vti"))
+    assert np.isfinite(d["U"]).all()
+    assert abs(d["U"][0, 16, 64, 0] - 0.02) < 0.01
+    log = open(tmp_path / "output" / "case_Log_P00_00000000.csv").read().splitlines()
+    assert log[0].startswith('"Iteration"') and len(log) == 1 + 4
+    assert float(log[-1].split(",")[0]) == 100
+
+
+def test_xpath_edits_and_stop(tmp_path):
+    s = run_case(tmp_path, KARMAN, edits=["Model/Param[@name='Viscosity']/@value", "=", "0.1",
+                                          "Solve", "@Iterations", "=", "60"])
+    assert s.lattice.get_setting("Viscosity") == pytest.approx(0.1)
+    assert s.iter == 60
+
+
+def test_checkpoint_restart_bitwise(tmp_path):
+    xml = KARMAN.replace('<Solve Iterations="100"/>',
+                         '<Solve Iterations="40"><SaveCheckpoint Iterations="20" keep="2"/></Solve>')
+    s = run_case(tmp_path, xml)
+    ref = s.lattice.fields_interior().clone()
+    rst = tmp_path / "output" / "case_restart_00000020.xml"
+    assert rst.exists()
+    # restart from iteration 20 and continue 20 iterations
+    root = ET.parse(rst).getroot()
+    for e in list(root):
+        if e.tag in ("VTK", "Log", "Failcheck"):
+            root.remove(e)
+    root.find("Solve").set("Iterations", "20")
+    for c in list(root.find("Solve")):
+        root.find("Solve").remove(c)
+    s2 = Solver("d2q9", root, conffile=str(tmp_path / "case2.xml"), device="cpu")
+    s2.run()
+    assert s2.iter == 40
+    assert (s2.lattice.fields_interior() == ref).all()
+
+
+def test_failcheck_stops_on_nan(tmp_path):
+    xml = KARMAN.replace('<Param name="Viscosity" value="0.05"/>', '<Param name="Viscosity" value="-0.1666"/>')
+    xml = xml.replace('<Failcheck Iterations="50"/>', '<Failcheck Iterations="10"/>')
+    s = run_case(tmp_path, xml)
+    assert s.iter < 100
+
+
+def test_cli_module(tmp_path):
+    (tmp_path / "k.xml").write_text(KARMAN.replace('Iterations="100"', 'Iterations="10"'))
+    r = subprocess.run([sys.executable, "-m", "tclb_amd", "d2q9", "k.xml", "--device", "cpu"], cwd=tmp_path,
+                       capture_output=True, text=True, env={**os.environ, "PYTHONPATH": os.getcwd() + ":" +
+                                                            os.path.dirname(os.path.dirname(os.path.abspath(__file__)))})
+    assert r.returncode == 0, r.stderr
