@@ -1,0 +1,64 @@
+"""Worker for multi-process (gloo, CPU) tests of the decomposition + halo path."""
+import os
+import sys
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def setup_flags(lat):
+    m = lat.model
+    nx = lat.shape[0]
+    fl = np.full((lat.NZ, lat.NY, nx), m.node_type("MRT").value, dtype=np.uint32)
+    if m.name == "d3q27":
+        # walls at global y = 0 and y = gny-1 (y not split in 3-D)
+        fl[:, lat.gy + 0, :] = m.node_type("Wall").value
+        fl[:, lat.gy + lat.shape[1] - 1, :] = m.node_type("Wall").value
+    return fl
+
+
+def run_case(model, shape, steps, comm, overlap=None):
+    from tclb_amd.lattice import Lattice
+    lat = Lattice(model, shape, comm=comm, overlap=overlap)
+    lat.set_flags(setup_flags(lat))
+    if model == "d3q27":
+        lat.set_setting("nu", 0.05)
+        lat.set_setting("ForceX", 1e-4)
+        lat.set_setting("Velocity", 0.01)
+    else:
+        lat.set_setting("Viscosity", 0.05)
+        lat.set_setting("VelocityX", 0.01)
+        lat.set_setting("GravitationX", 1e-5)
+    lat.init()
+    # deterministic perturbation in global coordinates
+    f = lat.fields_interior().clone()
+    ox, oy, oz = lat.slab.offset
+    nx, ny, nz = lat.shape
+    Z, Y, X = np.meshgrid(np.arange(oz, oz + nz), np.arange(oy, oy + ny), np.arange(nx), indexing="ij")
+    pert = 1 + 0.01 * np.sin(0.3 * X + 0.7 * Y + 1.1 * Z)
+    lat.set_fields_interior(f * torch.from_numpy(pert)[None])
+    lat.iterate(steps)
+    return lat
+
+
+def worker(rank, world, port, model, shape, steps, out, overlap):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from tclb_amd.parallel.comm import TorchDistComm
+    comm = TorchDistComm()
+    lat = run_case(model, shape, steps, comm, overlap=overlap)
+    parts = comm.gather_objects((lat.slab.lo, lat.fields_interior().numpy(), lat.globals))
+    if rank == 0:
+        axis = 1 if lat.slab.axis == 2 else 2  # concat axis in (nf, z, y, x)
+        parts.sort(key=lambda p: p[0])
+        full = np.concatenate([p[1] for p in parts], axis=axis)
+        np.save(out, full)
+        import json
+        with open(out + ".json", "w") as f:
+            json.dump(parts[0][2], f)
+    dist.barrier()
+    dist.destroy_process_group()
