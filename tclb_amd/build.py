@@ -27,8 +27,19 @@ CXX = os.environ.get("TCLB_CXX", "g++")
 ARCH = os.environ.get("TCLB_OFFLOAD_ARCH", "gfx950")
 
 
-def lib_path(model: str, kind: str) -> str:
-    return os.path.join(LIB, f"libtclb_{model}_{kind}.so")
+# build variants (extra compile definitions), used for on-device A/B tuning
+VARIANTS = {
+    "": [],
+    "nt": ["-DTCLB_NT_LOAD=1", "-DTCLB_NT_STORE=1"],
+    "ntst": ["-DTCLB_NT_STORE=1"],
+    "ntld": ["-DTCLB_NT_LOAD=1"],
+}
+DEFAULT_VARIANT = os.environ.get("TCLB_VARIANT", "")
+
+
+def lib_path(model: str, kind: str, variant: str = "") -> str:
+    suffix = f"_{variant}" if variant else ""
+    return os.path.join(LIB, f"libtclb_{model}_{kind}{suffix}.so")
 
 
 def _hash_inputs(paths: Iterable[str], extra: str = "") -> str:
@@ -49,16 +60,18 @@ def _deps(model_dir: str, dynamics: Optional[str]) -> List[str]:
     return deps
 
 
-def _cmd(kind: str, src: str, out: str, gen_dir: str) -> List[str]:
+def _cmd(kind: str, src: str, out: str, gen_dir: str, variant: str = "") -> List[str]:
     incs = ["-I", os.path.join(CSRC, "include"), "-I", os.path.join(CSRC, "models"), "-I", gen_dir]
     if kind == "hip":
         return [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-                "-munsafe-fp-atomics", "-Wno-unused-result", "-Wno-pass-failed", *incs, src, "-o", out]
+                "-munsafe-fp-atomics", "-Wno-unused-result", "-Wno-pass-failed", *VARIANTS[variant], *incs,
+                src, "-o", out]
     return [CXX, "-O3", "-std=c++17", "-fPIC", "-shared", "-fopenmp", "-fno-strict-aliasing",
             "-Wno-unused-variable", *incs, src, "-o", out]
 
 
-def build_model(name: str, kinds=("cpu", "hip"), force: bool = False, verbose: bool = False) -> Dict[str, str]:
+def build_model(name: str, kinds=("cpu", "hip"), force: bool = False, verbose: bool = False,
+                variant: str = "") -> Dict[str, str]:
     model = registry.get(name)
     paths = emit_model(model)
     os.makedirs(LIB, exist_ok=True)
@@ -66,9 +79,10 @@ def build_model(name: str, kinds=("cpu", "hip"), force: bool = False, verbose: b
     for kind in kinds:
         if kind == "hip" and not os.path.exists(HIPCC):
             continue
-        target = lib_path(name, kind)
+        v = variant if kind == "hip" else ""
+        target = lib_path(name, kind, v)
         src = paths[kind]
-        cmd = _cmd(kind, src, target, paths["dir"])
+        cmd = _cmd(kind, src, target, paths["dir"], v)
         h = _hash_inputs(_deps(paths["dir"], model.dynamics), " ".join(cmd))
         stamp = target + ".hash"
         if not force and os.path.exists(target) and os.path.exists(stamp) and open(stamp).read() == h:
@@ -84,7 +98,7 @@ def build_model(name: str, kinds=("cpu", "hip"), force: bool = False, verbose: b
         with open(stamp, "w") as f:
             f.write(h)
         if verbose:
-            print(f"[tclb build] {name} [{kind}] {time.time() - t0:.1f}s", flush=True)
+            print(f"[tclb build] {name} [{kind}{'/' + v if v else ''}] {time.time() - t0:.1f}s", flush=True)
         out[kind] = target
     return out
 

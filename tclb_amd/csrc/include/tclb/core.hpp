@@ -90,6 +90,32 @@ struct Addr {
   }
 };
 
+// Streaming loads/stores.  Every population is read once and written once per step,
+// so non-temporal hints keep the 4 MB/XCD L2 for the x-misaligned neighbour lines.
+// Selected at build time (-DTCLB_NT_LOAD=1 / -DTCLB_NT_STORE=1), A/B-tested on MI355X.
+#ifndef TCLB_NT_LOAD
+#define TCLB_NT_LOAD 0
+#endif
+#ifndef TCLB_NT_STORE
+#define TCLB_NT_STORE 0
+#endif
+template <class T>
+TCLB_FN T load_stream(const T* p) {
+#if TCLB_GPU && TCLB_NT_LOAD && defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_nontemporal_load(p);
+#else
+  return *p;
+#endif
+}
+template <class T>
+TCLB_FN void store_stream(T* p, T v) {
+#if TCLB_GPU && TCLB_NT_STORE && defined(__HIP_DEVICE_COMPILE__)
+  __builtin_nontemporal_store(v, p);
+#else
+  *p = v;
+#endif
+}
+
 template <class T>
 TCLB_FN T tmax(T a, T b) { return a > b ? a : b; }
 template <class T>

@@ -106,8 +106,10 @@ inline void launch_shape(const Launch& L, dim3& grid, dim3& block) {
     bx = 64;
     while (bx < 256 && bx < w) bx *= 2;
   }
+  if (bx > 256) bx = 256;
   int by = L.block_y > 0 ? L.block_y : 256 / bx;
   if (by < 1) by = 1;
+  if (bx * by > 256) by = 256 / bx;  // kernels are compiled with __launch_bounds__(256)
   block = dim3(bx, by, 1);
   grid = dim3((w + bx - 1) / bx, (h + by - 1) / by, d);
 }

@@ -54,7 +54,7 @@ def _runs(idx: Sequence[int]) -> List[Tuple[int, int]]:
 class Lattice:
     def __init__(self, model, shape: Tuple[int, int, int], device: Optional[torch.device] = None,
                  precision: str = "double", comm: Optional[Comm] = None, block: Tuple[int, int] = (0, 0),
-                 overlap: Optional[bool] = None):
+                 overlap: Optional[bool] = None, variant: Optional[str] = None):
         self.model: Model = registry.get(model) if isinstance(model, str) else model.finalize()
         m = self.model
         self.comm = comm or LoopbackComm()
@@ -106,7 +106,7 @@ class Lattice:
         self.block = block
         self.overlap = self.comm.distributed if overlap is None else overlap
         kind = "hip" if self.is_gpu else "cpu"
-        self.lib = abi.load(m.name, kind)
+        self.lib = abi.load(m.name, kind, variant=variant)
         # halo field sets: fields read from below (stencil min < 0) / above (max > 0) along axis
         self.halo_lo = [i for i, f in enumerate(m.fields) if f.stencil[ax][0] < 0]
         self.halo_hi = [i for i, f in enumerate(m.fields) if f.stencil[ax][1] > 0]

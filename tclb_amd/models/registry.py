@@ -42,3 +42,5 @@ def get(name: str) -> Model:
 # ---- catalog ---------------------------------------------------------------------
 register("d3q27", ".flow.d3q27")
 register("d2q9", ".flow.d2q9")
+register("d3q19", ".flow.d3q19")
+register("d2q9_SRT", ".flow.d2q9_srt")

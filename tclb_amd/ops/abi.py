@@ -90,15 +90,17 @@ _libs: Dict[tuple, ModelLib] = {}
 _lock = threading.Lock()
 
 
-def load(model: str, kind: str, build_if_missing: bool = True) -> ModelLib:
+def load(model: str, kind: str, build_if_missing: bool = True, variant: Optional[str] = None) -> ModelLib:
     from .. import build as B
-    key = (model, kind)
+    if variant is None:
+        variant = B.DEFAULT_VARIANT if kind == "hip" else ""
+    key = (model, kind, variant)
     with _lock:
         if key in _libs:
             return _libs[key]
-        path = B.lib_path(model, kind)
+        path = B.lib_path(model, kind, variant)
         if build_if_missing and (not os.path.exists(path) or os.environ.get("TCLB_REBUILD")):
-            B.build_model(model, kinds=(kind,))
+            B.build_model(model, kinds=(kind,), variant=variant)
         if not os.path.exists(path):
             raise KernelError(f"kernel library for model '{model}' [{kind}] not built: {path}")
         lib = ModelLib(model, kind, path)
