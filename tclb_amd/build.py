@@ -29,10 +29,11 @@ ARCH = os.environ.get("TCLB_OFFLOAD_ARCH", "gfx950")
 
 # build variants (extra compile definitions), used for on-device A/B tuning
 VARIANTS = {
-    "": [],
+    "": ["-DTCLB_NT_STORE=1"],          # default: non-temporal stores (A/B on MI355X: +2..7 %)
+    "plain": [],
     "nt": ["-DTCLB_NT_LOAD=1", "-DTCLB_NT_STORE=1"],
-    "ntst": ["-DTCLB_NT_STORE=1"],
     "ntld": ["-DTCLB_NT_LOAD=1"],
+    "noxs": ["-DTCLB_DEBUG_NO_XSHIFT", "-DTCLB_NT_STORE=1"],   # diagnostic: aligned-x ceiling
 }
 DEFAULT_VARIANT = os.environ.get("TCLB_VARIANT", "")
 

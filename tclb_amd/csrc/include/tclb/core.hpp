@@ -81,6 +81,9 @@ struct Addr {
     node = x + sy * (y + gy) + sz * (z + gz);
   }
   TCLB_FN int off(int dx, int dy, int dz) const {
+#ifdef TCLB_DEBUG_NO_XSHIFT
+    dx = 0;  // diagnostic build only: aligned-x ceiling of the access pattern (wrong physics)
+#endif
     int xx = dx == 0 ? x : wrap(x + dx, nx);
     int yy = y + dy;
     if (dy != 0 && gy == 0) yy = wrap(yy, ny);

@@ -99,12 +99,14 @@ __global__ void __launch_bounds__(256) k_quantity(const Launch L) {
   for (int c = 0; c < nc; c++) out[idx + (long long)c * L.qcomp] = o[c] * R(L.qscale);
 }
 
-inline void launch_shape(const Launch& L, dim3& grid, dim3& block) {
+// Default shapes from on-device A/B (profiles/r01_tune_*): fp64 storage 128x2, fp32 256x1.
+inline void launch_shape(const Launch& L, dim3& grid, dim3& block, int sbytes = 8) {
   const int w = L.xhi - L.xlo, h = L.yhi - L.ylo, d = L.zhi - L.zlo;
   int bx = L.block_x > 0 ? L.block_x : 0;
   if (bx == 0) {
+    const int bmax = sbytes >= 8 ? 128 : 256;
     bx = 64;
-    while (bx < 256 && bx < w) bx *= 2;
+    while (bx < bmax && bx < w) bx *= 2;
   }
   if (bx > 256) bx = 256;
   int by = L.block_y > 0 ? L.block_y : 256 / bx;
@@ -123,7 +125,7 @@ inline bool launch_one(const Launch& L, dim3 grid, dim3 block, hipStream_t s) {
 template <class Model, class R, class S, bool G, int... I>
 inline int run_stage_impl(const Launch& L, std::integer_sequence<int, I...>) {
   dim3 grid, block;
-  launch_shape(L, grid, block);
+  launch_shape(L, grid, block, (int)sizeof(S));
   if (grid.x == 0 || grid.y == 0 || grid.z == 0) return 0;
   hipStream_t s = (hipStream_t)L.stream;
   bool found = false;
@@ -142,7 +144,7 @@ inline int run_stage(const Launch& L) {
 template <class Model, class R, class S>
 inline int run_quantity(const Launch& L) {
   dim3 grid, block;
-  launch_shape(L, grid, block);
+  launch_shape(L, grid, block, (int)sizeof(S));
   if (grid.x == 0 || grid.y == 0 || grid.z == 0) return 0;
   k_quantity<Model, R, S><<<grid, block, 0, (hipStream_t)L.stream>>>(L);
   return (int)hipGetLastError();

@@ -23,7 +23,7 @@ def main():
     ap.add_argument("--model", default="d3q27")
     ap.add_argument("--size", type=int, default=512)
     ap.add_argument("--precision", default="double")
-    ap.add_argument("--variants", default=",nt,ntst,ntld")
+    ap.add_argument("--variants", default=",plain,nt,ntld")
     ap.add_argument("--blocks", default="256x1,128x2,64x4,128x1,64x2")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--rounds", type=int, default=3)
