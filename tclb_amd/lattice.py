@@ -222,9 +222,7 @@ class Lattice:
 
     # ------------------------------------------------------------------ actions
     def _saved_fields(self, stage) -> List[int]:
-        if stage.save_fields is None:
-            return list(range(self.nf))
-        return [i for i, f in enumerate(self.model.fields) if f.nicename in stage.save_fields or f.name in stage.save_fields]
+        return [i for i, f in enumerate(self.model.fields) if self.model.matches(f, stage.save_fields)]
 
     def run_action(self, name: str, glob: bool = False):
         m = self.model

@@ -27,8 +27,8 @@ from typing import Callable, Dict, List, Optional, Sequence, Tuple
 @dataclass
 class Field:
     name: str                      # C++ member name (e.g. "f[3]" or "psi")
-    group: str                     # member array / group
-    index: int                     # index inside group array (-1: scalar member)
+    group: str                     # group tag (stage load/save selection, VTK, checkpoints)
+    index: int                     # index inside member array (-1: scalar member named `array`)
     nicename: str                  # identifier-safe name, e.g. f3
     stencil: Tuple[Tuple[int, int], Tuple[int, int], Tuple[int, int]] = ((0, 0), (0, 0), (0, 0))
     comment: str = ""
@@ -37,7 +37,7 @@ class Field:
     default: float = 0.0
     shift: Optional[float] = None
     is_density: bool = False
-
+    array: str = ""                # C++ member: array name (index >= 0) or scalar name
 
 @dataclass
 class Density:
@@ -147,12 +147,11 @@ class Model:
                     parameter: bool = False, average: bool = False, default: float = 0.0,
                     shift: Optional[float] = None, comment: str = ""):
         """AddDensity (src/conf.R:65-102): a streamed population, pulled from (-dx,-dy,-dz)."""
-        grp, idx = self._split_name(name, group)
-        if group is not None and idx is None:
-            grp = group
+        arr, idx = self._split_name(name, None)
+        grp = group if group is not None else arr
         if idx is None:
-            idx = sum(1 for f in self.fields if f.group == grp)
-        f = Field(name=name, group=grp, index=idx, nicename=nicename(name),
+            arr, idx = name, -1
+        f = Field(name=name, group=grp, index=idx, nicename=nicename(name), array=arr,
                   stencil=((min(0, -dx), max(0, -dx)), (min(0, -dy), max(0, -dy)), (min(0, -dz), max(0, -dz))),
                   comment=comment, parameter=parameter, average=average, default=default, shift=shift,
                   is_density=True)
@@ -189,10 +188,11 @@ class Model:
                          (min(f.stencil[1][0], sy[0]), max(f.stencil[1][1], sy[1])),
                          (min(f.stencil[2][0], sz[0]), max(f.stencil[2][1], sz[1])))
             return f
-        grp, idx = self._split_name(name, group)
-        f = Field(name=name, group=grp if idx is not None else name, index=idx if idx is not None else -1,
-                  nicename=nicename(name), stencil=(sx, sy, sz), comment=comment, parameter=parameter,
-                  average=average, default=default)
+        arr, idx = self._split_name(name, None)
+        if idx is None:
+            arr, idx = name, -1
+        f = Field(name=name, group=group or arr, index=idx, nicename=nicename(name), array=arr,
+                  stencil=(sx, sy, sz), comment=comment, parameter=parameter, average=average, default=default)
         self._add_field(f)
         return f
 
@@ -241,10 +241,15 @@ class Model:
             return
         self.node_types.append(NodeType(name=name, group=group))
 
-    def add_stage(self, name: str, main: Optional[str] = None, load_densities: bool = True,
-                  save_fields: Optional[Sequence[str]] = None, read_fields: Optional[Sequence[str]] = None,
+    def add_stage(self, name: str, main: Optional[str] = None, load_densities=False,
+                  save_fields=False, read_fields: Optional[Sequence[str]] = None,
                   fixed_point: bool = False, particle: bool = False, init: bool = False):
-        """AddStage (src/conf.R:295-330)."""
+        """AddStage (src/conf.R:295-330): load_densities / save_fields are True (all), False
+        (none) or lists of field names / group tags (reference defaults: FALSE)."""
+        if save_fields is True:
+            save_fields = None
+        elif save_fields is False:
+            save_fields = []
         st = Stage(name=name, main=main or name, load_densities=load_densities,
                    save_fields=list(save_fields) if save_fields is not None else None,
                    read_fields=list(read_fields) if read_fields is not None else None,
@@ -332,7 +337,7 @@ class Model:
                 bad = reads - names
                 if bad:
                     raise ModelError(f"stage {st.name} reads unknown fields {sorted(bad)}")
-                saves = set(st.save_fields) if st.save_fields is not None else set(names)
+                saves = {f.nicename for f in self.fields if self.matches(f, st.save_fields)}
                 overl = reads & saves
                 if overl and not st.init and st.read_fields is not None:
                     # reading a field with a stencil while writing it in the same stage is a race
@@ -394,14 +399,22 @@ class Model:
         return None
 
     def group_arrays(self) -> Dict[str, int]:
-        """member arrays: group -> size (scalar members have size 0)."""
+        """C++ members: array name -> size (scalar members have size 0)."""
         out: Dict[str, int] = {}
         for f in self.fields:
             if f.index >= 0:
-                out[f.group] = max(out.get(f.group, 0), f.index + 1)
+                out[f.array] = max(out.get(f.array, 0), f.index + 1)
             else:
-                out.setdefault(f.group, 0)
+                out.setdefault(f.array, 0)
         return out
+
+    def matches(self, f: Field, spec) -> bool:
+        """stage load/save selection: True/None = all, False = none, list of names/groups"""
+        if spec is None or spec is True:
+            return True
+        if spec is False:
+            return False
+        return f.name in spec or f.nicename in spec or f.group in spec
 
     def halo(self) -> Tuple[int, int, int]:
         """max |stencil| per axis (reference BorderMargin, src/conf.R:1017-1023)."""

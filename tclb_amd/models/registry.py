@@ -44,3 +44,4 @@ register("d3q27", ".flow.d3q27")
 register("d2q9", ".flow.d2q9")
 register("d3q19", ".flow.d3q19")
 register("d2q9_SRT", ".flow.d2q9_srt")
+register("d2q9_ShanChen", ".multiphase.d2q9_shanchen")
