@@ -14,8 +14,8 @@ from .dsl import Model
 _MODELS: Dict[str, tuple] = {}
 
 
-def register(name: str, module: str, **kwargs):
-    _MODELS[name] = (module, kwargs)
+def register(name: str, module: str, builder: str = "build", **kwargs):
+    _MODELS[name] = (module, builder, kwargs)
 
 
 def names() -> List[str]:
@@ -29,9 +29,9 @@ def get(name: str) -> Model:
     if name not in _MODELS:
         raise KeyError(f"unknown model '{name}'; known: {', '.join(names())}")
     if name not in _cache:
-        mod, kw = _MODELS[name]
+        mod, builder, kw = _MODELS[name]
         m = importlib.import_module(mod, package=__package__)
-        model = m.build(**kw) if kw else m.build()
+        model = getattr(m, builder)(**kw)
         if model.name != name:
             model.name = name
         model.finalize()
@@ -45,3 +45,7 @@ register("d2q9", ".flow.d2q9")
 register("d3q19", ".flow.d3q19")
 register("d2q9_SRT", ".flow.d2q9_srt")
 register("d2q9_ShanChen", ".multiphase.d2q9_shanchen")
+register("diffusion2D", ".pde.pde2d", "build_diffusion")
+register("advection_diffusion2D", ".pde.pde2d", "build_advection_diffusion")
+register("advection_diffusion2D_fields", ".pde.pde2d", "build_advection_diffusion", fields=True)
+register("wave2D", ".pde.pde2d", "build_wave")

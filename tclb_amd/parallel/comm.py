@@ -50,7 +50,14 @@ class Comm:
 
 
 class LoopbackComm(Comm):
-    """Single rank: neighbour below and above are this rank (periodic)."""
+    """Single rank: neighbour below and above are this rank (periodic).
+
+    ``exercise_dist_path=True`` routes the halo through the multi-rank code path
+    (border/interior split, pack, exchange, unpack) with this rank as its own
+    neighbour — used to test that path on a single GPU."""
+
+    def __init__(self, exercise_dist_path: bool = False):
+        self.distributed = exercise_dist_path
 
     def start_halo(self, send_up, send_down, recv_below, recv_above):
         if send_up is not None:

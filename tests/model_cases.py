@@ -1,0 +1,48 @@
+"""Generic per-model set-up used by the catalog-wide tests (CPU smoke + HIP-vs-CPU)."""
+import numpy as np
+import torch
+
+from tclb_amd.lattice import Lattice
+from tclb_amd.models import registry
+
+SMALL_2D = (40, 24, 1)
+SMALL_3D = (24, 12, 10)
+
+
+def collision_value(m):
+    for g in ("COLLISION",):
+        for n in m.node_types:
+            if n.group == g:
+                return n.value
+    return 0
+
+
+def make_case(name, device="cpu", precision="double", shape=None, comm=None):
+    m = registry.get(name)
+    shape = shape or (SMALL_2D if m.dims == 2 else SMALL_3D)
+    lat = Lattice(name, shape, device=torch.device(device), precision=precision, comm=comm)
+    nx = shape[0]
+    fl = np.full((lat.NZ, lat.NY, nx), collision_value(m), dtype=np.uint32)
+    wall = m.node_type("Wall")
+    if wall is not None:
+        fl[:, :, 0] = wall.value   # x = 0 plane of walls (not on the decomposed axis)
+    lat.set_flags(fl)
+    return lat
+
+
+def perturb(lat, amp=0.01):
+    f = lat.fields_interior().clone()
+    ox, oy, oz = lat.slab.offset
+    nx, ny, nz = lat.shape
+    Z, Y, X = np.meshgrid(np.arange(oz, oz + nz), np.arange(oy, oy + ny), np.arange(nx), indexing="ij")
+    p = 1 + amp * np.sin(0.37 * X + 0.71 * Y + 1.13 * Z)
+    p = torch.from_numpy(p).to(f.device, f.dtype)
+    lat.set_fields_interior(f * p[None])
+
+
+def run(name, device="cpu", steps=3, precision="double", comm=None, shape=None):
+    lat = make_case(name, device, precision, shape=shape, comm=comm)
+    lat.init()
+    perturb(lat)
+    lat.iterate(steps)
+    return lat

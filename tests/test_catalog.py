@@ -1,0 +1,57 @@
+"""Catalog-wide checks: every registered model builds, initialises and iterates on the CPU
+executor with finite results; on a GPU box the HIP kernels must reproduce the CPU
+executor (fp64) for every model, and the multi-rank halo path (border/interior split,
+pack/exchange/unpack) must reproduce the loopback path."""
+import numpy as np
+import pytest
+import torch
+
+from model_cases import run
+from tclb_amd.models import registry
+from tclb_amd.parallel.comm import LoopbackComm
+
+MODELS = registry.names()
+needs_gpu = pytest.mark.skipif(not torch.cuda.is_available(), reason="no GPU")
+
+
+@pytest.mark.parametrize("name", MODELS)
+def test_model_cpu_smoke(name):
+    lat = run(name, "cpu", steps=3)
+    assert torch.isfinite(lat.fields_interior()).all()
+    for q in lat.model.quantities:
+        assert torch.isfinite(lat.quantity(q.name)).all(), q.name
+    for k, v in lat.globals.items():
+        assert np.isfinite(v), k
+
+
+@pytest.mark.gpu
+@needs_gpu
+@pytest.mark.parametrize("name", MODELS)
+def test_model_hip_matches_cpu(name):
+    a = run(name, "cuda", steps=3)
+    b = run(name, "cpu", steps=3)
+    assert a.lib.kind == "hip"
+    fa, fb = a.fields_interior().cpu(), b.fields_interior()
+    scale = fb.abs().max().item() + 1e-300
+    assert torch.allclose(fa, fb, atol=1e-11 * scale, rtol=1e-11), (fa - fb).abs().max().item()
+    for q in a.model.quantities:
+        qa, qb = a.quantity(q.name).cpu(), b.quantity(q.name)
+        s = qb.abs().max().item() + 1e-300
+        assert torch.allclose(qa, qb, atol=1e-10 * s, rtol=1e-10), q.name
+
+
+@pytest.mark.gpu
+@needs_gpu
+@pytest.mark.parametrize("name", ["d3q27", "d2q9", "d2q9_ShanChen"])
+def test_dist_path_on_gpu_matches_loopback(name):
+    a = run(name, "cuda", steps=4, comm=LoopbackComm(exercise_dist_path=True))
+    b = run(name, "cuda", steps=4, comm=LoopbackComm())
+    assert a.overlap and not b.overlap
+    assert torch.equal(a.fields_interior(), b.fields_interior())
+
+
+@pytest.mark.parametrize("name", ["d3q27", "d2q9_ShanChen"])
+def test_dist_path_on_cpu_matches_loopback(name):
+    a = run(name, "cpu", steps=4, comm=LoopbackComm(exercise_dist_path=True))
+    b = run(name, "cpu", steps=4, comm=LoopbackComm())
+    assert torch.equal(a.fields_interior(), b.fields_interior())
