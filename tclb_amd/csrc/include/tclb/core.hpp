@@ -60,6 +60,12 @@ struct Launch {
   long long qsy, qsz;      // quantity buffer strides (box-relative)
   int block_x, block_y;    // launch shape hint (GPU)
   int reserved0, reserved1;
+  // extension slots (model services): 0 = synthetic-turbulence modes, 1 = cuts (uint16
+  // [26][field]), 2 = particles (double[npart][PART_STRIDE]), 3 = particle forces
+  // accumulator (double[npart][6]), 4,5 = model-specific
+  const void* ext[6];
+  long long next[6];       // element counts of the ext slots
+  double time_shift;       // spare scalar
 };
 
 // Periodic wrap helper for non-decomposed axes.

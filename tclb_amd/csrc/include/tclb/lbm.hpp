@@ -116,7 +116,7 @@ TCLB_FN constexpr double zh_T(int ax, int sgn, int t) {
 }
 
 template <class L, int AX, int SGN, int MODE, class R>
-TCLB_FN void zouhe(R* f, bool pressure, R value, R& rho_out, R* J) {
+TCLB_FN void zouhe(R* f, bool pressure, R value, R& rho_out, R* J, const R* vt = nullptr) {
   R A = R(0);
   R B[3] = {R(0), R(0), R(0)};
   TCLB_UNROLL for (int i = 0; i < L::Q; i++) {
@@ -142,6 +142,10 @@ TCLB_FN void zouhe(R* f, bool pressure, R value, R& rho_out, R* J) {
     const double T = zh_T<L>(AX, SGN, t);
     if (MODE == ZH_REF) J[t] = B[t] * R(1.0 / (1.0 - T));
     else J[t] = -B[t] * R(1.0 / T);
+  }
+  if (vt != nullptr) {
+    TCLB_UNROLL for (int t = 0; t < L::D; t++)
+      if (t != AX) J[t] += rho * vt[t];
   }
   if (L::D < 3) J[2] = R(0);
   if (L::D < 2) J[1] = R(0);

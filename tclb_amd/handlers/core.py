@@ -641,3 +641,43 @@ class Control(GenericAction):
         for name, zone, t, v in self.series:
             s.lattice.set_setting(name, float(np.interp(s.iter, t, v)), zone=zone)
         return 0
+
+
+@register("SyntheticTurbulence")
+class SyntheticTurbulenceAction(Action):
+    """reference acSyntheticTurbulence (src/Handlers/acSyntheticTurbulence.cpp)"""
+
+    def _wn(self, name, default=None):
+        n = self.node
+        s = self.solver
+        val = default
+        if n.get(name + "WaveLength") is not None:
+            val = 1.0 / s.units.alt(n.get(name + "WaveLength"))
+        if n.get(name + "WaveNumber") is not None:
+            val = s.units.alt(n.get(name + "WaveNumber"))
+        if n.get(name + "WaveFrequency") is not None:
+            val = s.units.alt(n.get(name + "WaveFrequency")) * 8 * math.atan(1.0)
+        return val
+
+    def init(self):
+        super().init()
+        from ..utils.turbulence import SyntheticTurbulence
+        s = self.solver
+        nmodes = int(self.node.get("Modes", "100"))
+        spec = self.node.get("Spectrum", "Von Karman")
+        st = SyntheticTurbulence(seed=int(self.node.get("Seed", "0")))
+        if spec == "Von Karman":
+            main = self._wn("Main")
+            diff = self._wn("Diffusion")
+            if main is None or diff is None:
+                raise HandlerError("Must provide MainWaveNumber and DiffusionWaveNumber for Von Karman spectrum")
+            mx = self._wn("Shortest", 8 * math.atan(1) / 4)
+            mn = self._wn("Longest", main / 2)
+            st.set_von_karman(nmodes, main, diff, mn, mx, comm=s.comm)
+        elif spec == "One Wave":
+            st.set_one_wave(self._wn("Main"), comm=s.comm)
+        else:
+            raise HandlerError(f"Unknown spectrum {spec}")
+        s.lattice.set_turbulence(st.modes)
+        s.turbulence = st
+        return 0

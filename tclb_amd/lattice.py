@@ -115,6 +115,9 @@ class Lattice:
             self.set_setting(s.name, s.default, _init=True)
         self._L = self._base_launch()
         self.callbacks = []
+        self.turb_t = None
+        self.cuts = None
+        self.average_start = 0
 
     # ------------------------------------------------------------------ launch
     def _base_launch(self) -> abi.Launch:
@@ -144,6 +147,12 @@ class Lattice:
         L.nzones = self.zvals.shape[1]
         L.globals_ = self.globals_t.data_ptr()
         L.flags = self.flags.data_ptr()
+        if self.turb_t is not None:
+            L.ext[0] = self.turb_t.data_ptr()
+            L.next[0] = self.turb_t.shape[0]
+        if self.cuts is not None:
+            L.ext[1] = self.cuts.data_ptr()
+            L.next[1] = self.cuts.numel()
 
     def _stream(self) -> int:
         return torch.cuda.current_stream(self.device).cuda_stream if self.is_gpu else 0
@@ -156,6 +165,7 @@ class Lattice:
         L.stage = stage
         L.glob = 1 if glob else 0
         L.iter = self.iter
+        L.reserved1 = self.iter - self.average_start + 1
         L.stream = self._stream()
         nx, ny, nz = self.shape
         L.ylo, L.yhi, L.zlo, L.zhi = 0, ny, 0, nz
@@ -354,6 +364,10 @@ class Lattice:
         full[:, :, :, :nx] = cuts
         self.cuts = torch.from_numpy(full.view(np.int16)).to(self.device)
 
+    def set_turbulence(self, modes: np.ndarray):
+        """synthetic-turbulence modes (n, 7) -> device (Launch.ext[0])"""
+        self.turb_t = torch.as_tensor(np.ascontiguousarray(modes, dtype=np.float64)).to(self.device)
+
     def reset_average(self):
         """reset averaged fields (reference cbAveraging -> resetAverage, src/Lattice.cu.Rt:1360-1365)"""
         idx = [i for i, f in enumerate(self.model.fields) if f.average]
@@ -400,6 +414,7 @@ class Lattice:
         L.reserved0 = nc
         L.ylo, L.yhi, L.zlo, L.zhi = 0, ny, 0, nz
         L.iter = self.iter
+        L.reserved1 = max(1, self.iter - self.average_start)
         L.stream = self._stream()
         self.lib.quantity(L, self.prec)
         L.reserved0 = 0

@@ -49,3 +49,5 @@ register("diffusion2D", ".pde.pde2d", "build_diffusion")
 register("advection_diffusion2D", ".pde.pde2d", "build_advection_diffusion")
 register("advection_diffusion2D_fields", ".pde.pde2d", "build_advection_diffusion", fields=True)
 register("wave2D", ".pde.pde2d", "build_wave")
+register("d3q27_cumulant", ".flow.d3q27_cumulant")
+register("d3q27_cumulant_AVG_IB_SMAG", ".flow.d3q27_cumulant", avg=True, ib=True, smag=True)

@@ -47,6 +47,9 @@ class Launch(ctypes.Structure):
         ("qsz", ctypes.c_longlong),
         ("block_x", ctypes.c_int), ("block_y", ctypes.c_int),
         ("reserved0", ctypes.c_int), ("reserved1", ctypes.c_int),
+        ("ext", ctypes.c_void_p * 6),
+        ("next", ctypes.c_longlong * 6),
+        ("time_shift", ctypes.c_double),
     ]
 
 

@@ -11,6 +11,8 @@ CASES = {
     "d3q19": ((4, 18, 4), {"ForceX": 1e-6}, "nu"),
     "d2q9": ((4, 18, 1), {"GravitationX": 1e-6}, "Viscosity"),
     "d2q9_SRT": ((4, 18, 1), {"GravitationX": 1e-6}, "nu"),
+    "d3q27_cumulant": ((4, 18, 4), {"ForceX": 1e-6}, "nu"),
+    "d3q27_cumulant_AVG_IB_SMAG": ((4, 18, 4), {"ForceX": 1e-6}, "nu"),
 }
 
 
