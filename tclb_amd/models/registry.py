@@ -51,3 +51,4 @@ register("advection_diffusion2D_fields", ".pde.pde2d", "build_advection_diffusio
 register("wave2D", ".pde.pde2d", "build_wave")
 register("d3q27_cumulant", ".flow.d3q27_cumulant")
 register("d3q27_cumulant_AVG_IB_SMAG", ".flow.d3q27_cumulant", avg=True, ib=True, smag=True)
+register("d3q19_heat", ".heat.d3q19_heat")
