@@ -125,6 +125,70 @@ TCLB_FN void store_stream(T* p, T v) {
 #endif
 }
 
+// ---------------------------------------------------------------------------
+// Particles coupled to the lattice (reference Particle.hpp / RemoteForceInterface).
+// Device record (double): pos[3] vel[3] angvel[3] rad  -> PART_STRIDE = 10, in Launch.ext[2];
+// force/moment accumulators double[n][6] in Launch.ext[3].
+// ---------------------------------------------------------------------------
+constexpr int PART_STRIDE = 10;
+
+template <class R>
+struct ParticleS {
+  vec3<R> cvel, diff, force, moment;
+  R rad, dist;
+  int i;
+  TCLB_FN void init(const double* P, int i_, R x, R y, R z) {
+    i = i_;
+    const double* p = P + (long long)i * PART_STRIDE;
+    rad = R(p[9]);
+    diff.x = x - R(p[0]); diff.y = y - R(p[1]); diff.z = z - R(p[2]);
+    dist = sqrt(diff.x * diff.x + diff.y * diff.y + diff.z * diff.z);
+    const R wx = R(p[6]), wy = R(p[7]), wz = R(p[8]);
+    cvel.x = R(p[3]) + wy * diff.z - wz * diff.y;
+    cvel.y = R(p[4]) + wz * diff.x - wx * diff.z;
+    cvel.z = R(p[5]) + wx * diff.y - wy * diff.x;
+    force.x = force.y = force.z = R(0);
+    moment.x = moment.y = moment.z = R(0);
+  }
+  TCLB_FN bool in() const { return dist < rad; }
+  TCLB_FN void applyForce(vec3<R> f) {
+    force.x += f.x; force.y += f.y; force.z += f.z;
+    moment.x -= f.y * diff.z - f.z * diff.y;
+    moment.y -= f.z * diff.x - f.x * diff.z;
+    moment.z -= f.x * diff.y - f.y * diff.x;
+  }
+};
+
+// Flush one particle's force/moment contribution of this node.  On the GPU, when the
+// whole wavefront is active the 6 values are reduced across the wave first (one atomic
+// per value per wave, reference WARP_SYNC); otherwise each contributing lane adds.
+template <class R>
+TCLB_FN void particle_flush(double* acc, const ParticleS<R>& p) {
+  double v[6] = {(double)p.force.x, (double)p.force.y, (double)p.force.z,
+                 (double)p.moment.x, (double)p.moment.y, (double)p.moment.z};
+  double* a = acc + (long long)p.i * 6;
+#if TCLB_GPU && defined(__HIP_DEVICE_COMPILE__)
+  const unsigned long long act = __ballot(1);
+  if (act == ~0ull) {
+    const int lane = __lane_id();
+    TCLB_UNROLL for (int k = 0; k < 6; k++) {
+      double s = v[k];
+      TCLB_UNROLL for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+      if (lane == 0 && s != 0.0) unsafeAtomicAdd(a + k, s);
+    }
+  } else {
+    TCLB_UNROLL for (int k = 0; k < 6; k++)
+      if (v[k] != 0.0) unsafeAtomicAdd(a + k, v[k]);
+  }
+#else
+  for (int k = 0; k < 6; k++)
+    if (v[k] != 0.0) {
+#pragma omp atomic
+      a[k] += v[k];
+    }
+#endif
+}
+
 template <class T>
 TCLB_FN T tmax(T a, T b) { return a > b ? a : b; }
 template <class T>

@@ -681,3 +681,54 @@ class SyntheticTurbulenceAction(Action):
         s.lattice.set_turbulence(st.modes)
         s.turbulence = st
         return 0
+
+
+@register("RemoteForceInterface")
+class RemoteForceInterface(Action):
+    """reference acRemoteForceInterface (src/Handlers/acRemoteForceInterface.cpp): connects
+    the lattice to a particle integrator.  Supported integrator: SIMPLEPART (built-in,
+    in-process; configuration from the <SimplePart> child as in the reference)."""
+
+    def init(self):
+        super().init()
+        from ..particles import SimplePart
+        s = self.solver
+        integ = (self.node.get("integrator") or "").upper()
+        if integ not in ("SIMPLEPART", "BUILTIN"):
+            raise HandlerError(f"RemoteForceInterface integrator '{integ}' not available (use SIMPLEPART)")
+        sp = SimplePart()
+        u = s.units
+        off = [u.alt(s.config_tree.find("Geometry").get("p" + a, "0")) for a in "xyz"]
+        cfg = self.node.find("SimplePart")
+        lm, ls, lkg = u.alt("1m"), u.alt("1s"), u.alt("1kg")
+        if cfg is not None:
+            for a, d in (("ax", 0), ("ay", 1), ("az", 2)):
+                if cfg.get(a) is not None:
+                    sp.acc[d] = float(cfg.get(a)) * lm / ls ** 2
+            for c in cfg:
+                if c.tag == "Particle":
+                    x = [float(c.get(a, "0")) * lm - off[i] for i, a in enumerate("xyz")]
+                    v = [float(c.get("v" + a, "0")) * lm / ls for a in "xyz"]
+                    w = [float(c.get("omega" + a, "0")) / ls for a in "xyz"]
+                    r = float(c.get("r")) * lm
+                    mass = float(c.get("m")) * lkg if c.get("m") else None
+                    if c.get("log", "n").lower() in ("y", "yes", "true", "1"):
+                        sp.logged.append(sp.n)
+                    sp.add(x, r, v, w, mass)
+                elif c.tag == "Periodic":
+                    for i, a in enumerate("xyz"):
+                        if c.get(a) is not None:
+                            sp.periodic[i] = True
+                            sp.period[i] = float(c.get(a)) * lm
+                elif c.tag == "Log":
+                    sp.log_every = int(c.get("Iterations", "1"))
+                    sp.log_rotation = c.get("rotation", "false").lower() in ("true", "1")
+                    sp.log_path = c.get("name") or (s.outpath + "_SP_Log.csv")
+        for c in self.node:
+            if c.tag == "Particle":   # shorthand: particles directly under the element (lattice units)
+                sp.add([float(c.get(a, "0")) for a in "xyz"], float(c.get("r")),
+                       [float(c.get("v" + a, "0")) for a in "xyz"], fixed=c.get("fixed", "false") == "true")
+        s.lattice.particles = sp
+        s.particles = sp
+        log.output(f"RemoteForceInterface: {sp.n} particle(s) with built-in SIMPLEPART integrator")
+        return 0

@@ -117,6 +117,7 @@ class Lattice:
         self.callbacks = []
         self.turb_t = None
         self.cuts = None
+        self.particles = None     # ParticleSystem with pre_stage/post_stage/step hooks
         self.average_start = 0
 
     # ------------------------------------------------------------------ launch
@@ -251,6 +252,8 @@ class Lattice:
             st = m.stage(sname)
             inp = src if k == 0 else dst
             fields = self._saved_fields(st)
+            if st.particle and self.particles is not None:
+                self.particles.pre_stage(self)
             if self.overlap and n > 2 * g:
                 self._launch_stage(si, inp, dst, glob, (0, g))
                 self._launch_stage(si, inp, dst, glob, (n - g, n))
@@ -260,6 +263,10 @@ class Lattice:
             else:
                 self._launch_stage(si, inp, dst, glob)
                 self._halo_finish(self._halo_start(dst, fields))
+            if st.particle and self.particles is not None:
+                self.particles.post_stage(self)
+                if name != "Init":
+                    self.particles.step(self)
         self.cur = 1 - self.cur
         if glob:
             self._reduce_globals()

@@ -1,0 +1,94 @@
+"""auto — generic raw-moment LBM on D3Q27 or D3Q19 with MRT / BGK / TRT collision and an
+optional particle-coupling stage (CalcF).  Reference: models/flow/auto/Dynamics.R,
+Dynamics.c.Rt (OPT="d3q19*part*(TRT+BGK+WMRT)*FMT*HiOrd*autosym").
+
+Deviation (documented): with ``part`` the coupling force field (fx,fy,fz) written by
+the particle stage is added to the momentum in the collision (ForceX + fx), so the
+fluid feels the particles (two-way coupling); the reference variant only reports it."""
+import numpy as np
+import sympy as sp
+
+from ..dsl import Model
+from ...emit.blocks import dense_transform, exprs_function
+from ...emit.symbolic import mrt_eq
+
+CV = (0, 1, -1)
+
+
+def lattice(q19: bool):
+    P = [(a, b, c) for c in range(3) for b in range(3) for a in range(3)]
+    U = [(CV[a], CV[b], CV[c]) for a, b, c in P]
+    sel = [sum(abs(v) for v in u) < 3 for u in U] if q19 else [True] * 27
+    P = [p for p, s in zip(P, sel) if s]
+    U = np.array([u for u, s in zip(U, sel) if s])
+    return P, U
+
+
+def build(q19: bool = False, part: bool = False, coll: str = "MRT") -> Model:
+    name = "auto"
+    m = Model(name, dims=3, family="flow", reference="models/flow/auto",
+              description=f"raw-moment {'D3Q19' if q19 else 'D3Q27'} LBM, {coll} collision"
+                          f"{', particle coupling' if part else ''}")
+    P, U = lattice(q19)
+    Q = len(U)
+    for k in range(Q):
+        m.add_density(f"f[{k}]", int(U[k, 0]), int(U[k, 1]), int(U[k, 2]), group="f",
+                      comment="density f%d%d%d" % P[k])
+    for n in ("fx", "fy", "fz", "sol"):
+        m.add_density(n, 0, 0, 0, group="Force", parameter=True)
+    m.add_quantity("P", unit="Pa")
+    m.add_quantity("U", unit="m/s", vector=True)
+    m.add_quantity("Solid", unit="1")
+    m.add_quantity("F", unit="N/m3", vector=True)
+    m.add_setting("Viscosity", default=0.16666666, comment="Viscosity")
+    m.add_setting("Magic", default=3 / 16, comment="Magic parameter")
+    m.add_setting("Velocity", default="0m/s", comment="Inlet velocity", zonal=True, unit="m/s")
+    m.add_setting("Pressure", default="0Pa", comment="Inlet pressure", zonal=True, unit="Pa")
+    m.add_setting("Turbulence", comment="Turbulence intensity", zonal=True)
+    m.add_setting("GalileanCorrection", default=1.0, comment="Galilean correction term")
+    for a in "XYZ":
+        m.add_setting(f"Force{a}", default=0, comment=f"Force {a}")
+    m.add_global("Flux", comment="Volume flux", unit="m3/s")
+    m.add_global("Drag", comment="Force exerted on body in X-direction", unit="N")
+    m.add_global("Lift", comment="Force exerted on body in Z-direction", unit="N")
+    m.add_global("Lateral", comment="Force exerted on body in Y-direction", unit="N")
+    for n in ["WVelocityTurbulent", "NVelocity", "SVelocity", "NPressure", "SPressure"]:
+        m.add_node_type(n, "BOUNDARY")
+    m.add_node_type("Body", "BODY")
+    if part:
+        m.add_stage("BaseIteration", "Run", save_fields=["f"], load_densities=["f", "Force"])
+        m.add_stage("BaseInit", "Init", save_fields=["f", "Force"])
+        m.add_stage("CalcF", "CalcF", save_fields=["Force"], load_densities=["f"], particle=True)
+        m.add_action("Iteration", ["BaseIteration", "CalcF"])
+        m.add_action("Init", ["BaseInit", "CalcF"])
+    for n in ["EPressure", "EVelocity", "Wall", "WPressure", "WVelocity"]:
+        m.add_node_type(n, "BOUNDARY")
+    m.add_node_type("MRT", "COLLISION")
+    m.options = {"d3q19": q19, "part": part, "TRT": coll == "TRT", "BGK": coll == "BGK", "WMRT": False}
+
+    raw = mrt_eq(U, orthogonal=False)
+    M = sp.eye(Q) if coll == "BGK" else raw.mat
+    eq = mrt_eq(U, mat=M) if coll == "BGK" else raw
+    orders = [int(o) for o in eq.order]
+
+    def blocks(_m):
+        om = []
+        for o in orders:
+            if o < 2:
+                om.append("1")            # conserved
+            elif coll == "TRT" and o % 2 == 1:
+                om.append("2")            # omega2
+            elif coll == "MRT" and o > 2:
+                om.append("1")            # relaxed to equilibrium
+            else:
+                om.append("0")            # omega
+        out = [f"  TCLB_FN static constexpr int om_kind(int k) {{ constexpr int o[{Q}] = {{{', '.join(om)}}}; return o[k]; }}"]
+        out.append(dense_transform("am_moments", eq.mat, Q, Q, "m = f . M"))
+        out.append(dense_transform("am_inverse", eq.mat.inv(), Q, Q, "f = m . M^-1"))
+        out.append(exprs_function("am_req", ["rho", "Jx", "Jy", "Jz"], eq.Req))
+        out.append(exprs_function("am_feq", ["rho", "Jx", "Jy", "Jz"], eq.feq))
+        return "\n".join(out)
+    m.add_codegen(blocks)
+    m.defines["AUTO_Q"] = str(Q)
+    m.set_dynamics("flow/auto.inc")
+    return m

@@ -52,3 +52,13 @@ register("wave2D", ".pde.pde2d", "build_wave")
 register("d3q27_cumulant", ".flow.d3q27_cumulant")
 register("d3q27_cumulant_AVG_IB_SMAG", ".flow.d3q27_cumulant", avg=True, ib=True, smag=True)
 register("d3q19_heat", ".heat.d3q19_heat")
+register("auto", ".flow.auto")
+register("auto_d3q19", ".flow.auto", q19=True)
+register("auto_d3q19_BGK", ".flow.auto", q19=True, coll="BGK")
+register("auto_d3q19_TRT", ".flow.auto", q19=True, coll="TRT")
+register("auto_d3q19_part", ".flow.auto", q19=True, part=True)
+register("auto_d3q19_part_BGK", ".flow.auto", q19=True, part=True, coll="BGK")
+register("auto_d3q19_part_TRT", ".flow.auto", q19=True, part=True, coll="TRT")
+register("auto_part", ".flow.auto", part=True)
+register("auto_BGK", ".flow.auto", coll="BGK")
+register("auto_TRT", ".flow.auto", coll="TRT")
