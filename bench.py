@@ -56,10 +56,15 @@ def main():
     ap.add_argument("--block", default="0,0")
     ap.add_argument("--no-overlap", action="store_true")
     ap.add_argument("--cpu", action="store_true")
+    ap.add_argument("--loopback-dist", action="store_true",
+                    help="1 rank through the multi-rank path (border/interior split + pack/unpack)")
     a = ap.parse_args()
 
     use_gpu = torch.cuda.is_available() and not a.cpu
     comm = init_distributed_from_env("cuda" if use_gpu else "cpu")
+    if a.loopback_dist and comm.size == 1:
+        from tclb_amd.parallel.comm import LoopbackComm
+        comm = LoopbackComm(exercise_dist_path=True)
     rank, world = comm.rank, comm.size
     if use_gpu:
         local = int(os.environ.get("LOCAL_RANK", "0"))
