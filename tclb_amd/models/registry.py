@@ -62,3 +62,4 @@ register("auto_d3q19_part_TRT", ".flow.auto", q19=True, part=True, coll="TRT")
 register("auto_part", ".flow.auto", part=True)
 register("auto_BGK", ".flow.auto", coll="BGK")
 register("auto_TRT", ".flow.auto", coll="TRT")
+register("d3q19_les", ".flow.d3q19_les")

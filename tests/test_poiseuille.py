@@ -12,6 +12,10 @@ CASES = {
     "d2q9": ((4, 18, 1), {"GravitationX": 1e-6}, "Viscosity"),
     "d2q9_SRT": ((4, 18, 1), {"GravitationX": 1e-6}, "nu"),
     "d3q27_cumulant": ((4, 18, 4), {"ForceX": 1e-6}, "nu"),
+    "d3q19_les": ((4, 18, 4), {"ForceX": 1e-6}, "nu"),
+    "auto_d3q19_BGK": ((4, 18, 4), {"ForceX": 1e-6}, "Viscosity"),
+    "auto_d3q19_TRT": ((4, 18, 4), {"ForceX": 1e-6}, "Viscosity"),
+    "auto": ((4, 18, 4), {"ForceX": 1e-6}, "Viscosity"),
     "d3q27_cumulant_AVG_IB_SMAG": ((4, 18, 4), {"ForceX": 1e-6}, "nu"),
 }
 
