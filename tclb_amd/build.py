@@ -64,8 +64,13 @@ def _deps(model_dir: str, dynamics: Optional[str]) -> List[str]:
 def _cmd(kind: str, src: str, out: str, gen_dir: str, variant: str = "") -> List[str]:
     incs = ["-I", os.path.join(CSRC, "include"), "-I", os.path.join(CSRC, "models"), "-I", gen_dir]
     if kind == "hip":
+        # simplifycfg-sink-common=false: boundary-condition switch cases that permute
+        # the population array differ only in constant indices; sinking them into one
+        # block turns the indices into PHIs and demotes f[] to scratch (seen as 152 B/lane
+        # of scratch in the d3q27_cumulant fp64 kernel).
         return [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-                "-munsafe-fp-atomics", "-Wno-unused-result", "-Wno-pass-failed", *VARIANTS[variant], *incs,
+                "-munsafe-fp-atomics", "-mllvm", "-simplifycfg-sink-common=false",
+                "-Wno-unused-result", "-Wno-pass-failed", *VARIANTS[variant], *incs,
                 src, "-o", out]
     return [CXX, "-O3", "-std=c++17", "-fPIC", "-shared", "-fopenmp", "-fno-strict-aliasing",
             "-Wno-unused-variable", *incs, src, "-o", out]

@@ -1,0 +1,273 @@
+"""d3q27_pf_velocity — conservative phase-field (Allen-Cahn) + velocity-based
+pressure-evolution LBM for high-density-ratio two-phase flow: hydrodynamics on D3Q27
+(weighted-MRT in the 27-moment basis of the reference), interface on D3Q15 (or D3Q27
+with ``q27``).  Two distribution sets g (27) and h (15/27) + macroscopic/wall fields.
+
+Reference: models/multiphase/d3q27_pf_velocity/{Dynamics.R, model.R, Dynamics.c.Rt,
+Boundary.c.Rt}.  Implemented option subset: base, ``q27``, ``BGK`` (OutFlow, thermo,
+geometric, staircaseimp, isograd, tprec are not built in this round).
+
+Build-time derivations (sympy, replacing the reference's R polynomial algebra):
+* the 27x27 moment matrix M factorises as M = C . Mraw, Mraw the raw-monomial
+  tensor transform (3 axis passes) and C a 75-non-zero coefficient matrix, so the
+  moment transforms cost O(Q D) + 75 FMAs instead of 2 x 416;
+* equilibrium moments in the M basis (MRT_eq(..., mat=t(M)), Req[0] <- p);
+* stress of the non-equilibrium part (second moments of M^-1 m) as a 6-row map;
+* the 12 face boundary conditions (velocity / pressure on N,E,S,W,F,B) for g and h,
+  straight-line and CSE'd, exactly as Boundary.c.Rt:31-108 assembles them.
+"""
+import itertools
+
+import numpy as np
+import sympy as sp
+
+from ..dsl import Model
+from ...emit.blocks import dense_transform, exprs_function, tensor_raw_transform
+from ...emit.cprint import assign_block
+from ...emit.symbolic import mrt_eq
+
+# reference lattice.R ordering (g0..g26; h uses the first 15 or all 27)
+U27 = np.array([[0, 0, 0], [1, 0, 0], [-1, 0, 0], [0, 1, 0], [0, -1, 0], [0, 0, 1], [0, 0, -1],
+                [1, 1, 1], [-1, 1, 1], [1, -1, 1], [-1, -1, 1], [1, 1, -1], [-1, 1, -1], [1, -1, -1],
+                [-1, -1, -1], [1, 1, 0], [-1, 1, 0], [1, -1, 0], [-1, -1, 0], [1, 0, 1], [-1, 0, 1],
+                [1, 0, -1], [-1, 0, -1], [0, 1, 1], [0, -1, 1], [0, 1, -1], [0, -1, -1]])
+FACES = [("N", (0, 1, 0)), ("E", (1, 0, 0)), ("S", (0, -1, 0)), ("W", (-1, 0, 0)),
+         ("F", (0, 0, 1)), ("B", (0, 0, -1))]
+
+
+def moment_matrix() -> sp.Matrix:
+    """rows m0..m26 of model.R:16-44 evaluated on U27 (M[k, i])."""
+    X, Y, Z = sp.symbols("x y z")
+    a2 = X ** 2 + Y ** 2 + Z ** 2
+    h = sp.Rational(1, 2)
+    rows = [sp.Integer(1), X, Y, Z, X * Y, Y * Z, Z * X, 3 * X ** 2 - a2, Y ** 2 - Z ** 2, a2 - 1,
+            X * (3 * a2 - 5), Y * (3 * a2 - 5), Z * (3 * a2 - 5),
+            X * (Y ** 2 - Z ** 2), Y * (Z ** 2 - X ** 2), Z * (X ** 2 - Y ** 2), X * Y * Z,
+            h * (3 * a2 ** 2 - 7 * a2 + 2), (3 * a2 - 4) * (3 * X ** 2 - a2), (3 * a2 - 4) * (Y ** 2 - Z ** 2),
+            X * Y * (3 * a2 - 7), Y * Z * (3 * a2 - 7), Z * X * (3 * a2 - 7),
+            h * X * (9 * a2 ** 2 - 33 * a2 + 26), h * Y * (9 * a2 ** 2 - 33 * a2 + 26),
+            h * Z * (9 * a2 ** 2 - 33 * a2 + 26), h * (9 * a2 ** 3 - 36 * a2 ** 2 + 33 * a2 - 2)]
+    return sp.Matrix([[r.subs({X: int(u[0]), Y: int(u[1]), Z: int(u[2])}) for u in U27] for r in rows])
+
+
+def _raw_basis():
+    P = np.array([p for p in itertools.product(range(3), repeat=3)])[:, ::-1]   # a fastest
+    Mraw = sp.Matrix([[int(np.prod([int(u[d]) ** int(p[d]) for d in range(3)])) for u in U27] for p in P])
+    return P, Mraw
+
+
+def _bounce(U):
+    idx = {tuple(r): i for i, r in enumerate(U.tolist())}
+    return [idx[tuple((-np.array(r)).tolist())] for r in U.tolist()]
+
+
+def build(q27: bool = False, bgk: bool = False) -> Model:
+    m = Model("d3q27_pf_velocity", dims=3, family="multiphase", reference="models/multiphase/d3q27_pf_velocity",
+              description="phase-field (D3Q15/D3Q27 h) + velocity-based hydrodynamics (D3Q27 g), "
+                          "weighted-MRT, high density ratio")
+    Qh = 27 if q27 else 15
+    # ---- densities / fields (Dynamics.R:11-96, lattice.R)
+    for n in ("Init_UX_External", "Init_UY_External", "Init_UZ_External", "Init_PhaseField_External"):
+        m.add_density(n, 0, 0, 0, group="init", parameter=True)
+    for n in ("pnorm", "U", "V", "W"):
+        m.add_density(n, 0, 0, 0, group="Vel")
+    for n in ("nw_x", "nw_y", "nw_z"):
+        m.add_density(n, 0, 0, 0, group="nw")
+    m.add_density("IsSpecialBoundaryPoint", 0, 0, 0, group="solid_boundary")
+    m.add_quantity("SpecialBoundaryPoint", unit="1")
+    m.add_field("IsBoundary", stencil3d=1, group="solid_boundary")
+    m.add_field("PhaseF", stencil3d=1, group="PF")
+    for i, u in enumerate(U27):
+        m.add_density(f"g[{i}]", int(u[0]), int(u[1]), int(u[2]), group="g")
+    for i, u in enumerate(U27[:Qh]):
+        m.add_density(f"h[{i}]", int(u[0]), int(u[1]), int(u[2]), group="h")
+
+    save_initial_PF = ["PF", "Vel"]
+    save_initial = ["g", "h", "PF"]
+    save_iteration = ["g", "h", "Vel", "nw", "solid_boundary"]
+    load_iteration = ["g", "h", "Vel", "nw", "solid_boundary"]
+    load_phase = ["g", "h", "Vel", "nw", "solid_boundary"]
+    m.add_stage("PhaseInit", "Init", save_fields=save_initial_PF)
+    m.add_stage("BaseInit", "Init_distributions", save_fields=save_initial)
+    m.add_stage("calcPhase", "calcPhaseF", save_fields=["PhaseF"], load_densities=load_phase)
+    m.add_stage("BaseIter", "Run", save_fields=save_iteration, load_densities=load_iteration)
+    m.add_stage("InitFromFieldsStage", "InitFromFieldsStage", save_fields=save_initial_PF, load_densities=["init"])
+    m.add_stage("WallInit", "Init_wallNorm", save_fields=["nw", "solid_boundary"])
+    m.add_stage("calcWall", "calcWallPhase", save_fields=["PhaseF"], load_densities=["nw", "solid_boundary"])
+    m.add_stage("calcWallPhase_correction", "calcWallPhase_correction", save_fields=["PhaseF"],
+                load_densities=["nw", "solid_boundary"])
+    m.add_action("Iteration", ["BaseIter", "calcPhase", "calcWall", "calcWallPhase_correction"])
+    m.add_action("Init", ["PhaseInit", "WallInit", "calcWall", "calcWallPhase_correction", "BaseInit"])
+    m.add_action("InitFields", ["InitFromFieldsStage", "WallInit", "calcWall", "calcWallPhase_correction",
+                                "BaseInit"])
+    # ---- quantities
+    m.add_quantity("Rho", unit="kg/m3")
+    m.add_quantity("PhaseField", unit="1")
+    m.add_quantity("U", unit="m/s", vector=True)
+    m.add_quantity("P", unit="Pa")
+    m.add_quantity("Pstar", unit="1")
+    m.add_quantity("Normal", unit="1", vector=True)
+    m.add_quantity("IsItBoundary", unit="1")
+    # ---- settings (Dynamics.R:185-245)
+    S = m.add_setting
+    S("Density_h", comment="High density")
+    S("Density_l", comment="Low  density")
+    S("PhaseField_h", default=1, comment="PhaseField in Liquid")
+    S("PhaseField_l", default=0, comment="PhaseField gas")
+    S("PhaseField", comment="Initial PhaseField distribution", zonal=True)
+    S("IntWidth", default=4, comment="Anti-diffusivity coeff")
+    S("omega_phi", comment="one over relaxation time (phase field)")
+    S("M", default=0.02, comment="Mobility", omega_phi="1.0/(3*M+0.5)")
+    S("sigma", comment="surface tension")
+    S("force_fixed_iterator", default=2, comment="to resolve implicit relation of viscous force")
+    S("Washburn_start", default=0, comment="Start of washburn gas phase")
+    S("Washburn_end", default=0, comment="End of washburn gas phase")
+    S("radAngle", default="1.570796", comment="Contact angle in radians, can use units -> 90d where d=2pi/360",
+      zonal=True)
+    S("minGradient", default="1e-8", comment="if the phase gradient is less than this, set phase normals to zero")
+    S("RTI_Characteristic_Length", default=-999, comment="Use for RTI instability")
+    S("pseudo2D", default=0, comment="if 1, assume model is pseduo2D")
+    S("Radius", default=0.0, comment="Diffuse Sphere Radius")
+    S("CenterX", default=0.0, comment="Diffuse sphere center_x")
+    S("CenterY", default=0.0, comment="Diffuse sphere center_y")
+    S("CenterZ", default=0.0, comment="Diffuse sphere center_z")
+    S("BubbleType", default=1.0, comment="droplet(1.0) or bubble(-1.0)?!")
+    S("DonutTime", default=0.0, comment="Radius of a Torus - initialised to travel along x-axis")
+    S("Donut_h", default=0.0, comment="Half donut thickness, i.e. the radius of the cross-section")
+    S("Donut_D", default=0.0, comment="Dilation factor along the x-axis")
+    S("Donut_x0", default=0.0, comment="Position along x-axis")
+    S("HEIGHT", default=0, comment="Height of channel for 2D Poiseuille flow")
+    S("Uavg", default=0, zonal=True, comment="Average velocity of channel for 2D Poiseuille flow")
+    S("developedFlow", default=0, comment="set greater than 0 for fully developed flow in the domain (x-direction)")
+    S("developedPipeFlow", default=0, comment="set greater than 0 for fully developed pipe flow in the inlets")
+    S("developedPipeFlow_X", default=0,
+      comment="set greater than 0 for fully developed pipe flow in the domain (x-direction-only)")
+    S("pipeRadius", default=0, comment="radius of pipe for developed pipe flow")
+    S("pipeCentre_Y", default=0, comment="pipe centre Y co-ord for developed pipe flow")
+    S("pipeCentre_Z", default=0, comment="pipe centre Z co-ord for developed pipe flow")
+    S("tau_l", comment="relaxation time (low density fluid)")
+    S("tau_h", comment="relaxation time (high density fluid)")
+    S("tauUpdate", default=1, comment="Interpolation: 1-linear, 2- inverse, 3- dyn viscosity")
+    S("Viscosity_l", default=0.16666666, comment="kinematic viscosity", tau_l="(3*Viscosity_l)")
+    S("Viscosity_h", default=0.16666666, comment="kinematic viscosity", tau_h="(3*Viscosity_h)")
+    for a in "XYZ":
+        S(f"Velocity{a}", default=0.0, comment="inlet/outlet/init velocity", zonal=True)
+    S("Pressure", default=0.0, comment="inlet/outlet/init density", zonal=True)
+    for a in "XYZ":
+        S(f"Gravitation{a}", default=0.0, comment=f"applied (rho)*Gravitation{a}")
+    for a in "XYZ":
+        S(f"Buoyancy{a}", default=0.0, comment=f"applied (rho_h-rho)*Buoyancy{a}")
+    S("xyzTrack", default=1, comment="x<-1, y<-2, z<-3")
+    # ---- node types
+    for n in ("Centerline", "Spiketrack", "Saddletrack", "Bubbletrack"):
+        m.add_node_type(n, "ADDITIONALS")
+    # ---- globals (order of the reference)
+    m.add_global("InterfacePosition", op="MAX", comment="trackPosition")
+    m.add_global("InterfaceYTop", op="MAX", comment="Track top position of the interface in Y direction")
+    m.add_global("Vfront", comment="velocity infront of bubble")
+    m.add_global("Vback", comment="velocity behind bubble")
+    m.add_global("RTISpike", op="MAX", comment="SpikeTracker ")
+    m.add_global("RTIBubble", op="MAX", comment="BubbleTracker")
+    m.add_global("RTISaddle", op="MAX", comment="SaddleTracker")
+    m.add_global("XLocation", comment="tracking of x-centroid of the gas regions in domain", unit="m")
+    m.add_global("DropFront", op="MAX", comment="Highest location of droplet", unit="m")
+    m.add_node_type("Smoothing", "ADDITIONALS")
+    m.add_node_type("flux_nodes", "ADDITIONALS")
+    for f, _ in FACES:
+        m.add_node_type(f"{f}Velocity", "BOUNDARY")
+        m.add_node_type(f"{f}Pressure", "BOUNDARY")
+    for n in ("MovingWall_N", "MovingWall_S", "Solid", "Wall"):
+        m.add_node_type(n, "BOUNDARY")
+    m.add_node_type("BGK", "COLLISION")
+    m.add_node_type("MRT", "COLLISION")
+    for g, u in [("PressureLoss", "1mPa"), ("OutletFlux", "1m2/s"), ("InletFlux", "1m2/s"),
+                 ("TotalDensity", "1kg/m3"), ("KineticEnergy", "J"), ("GasTotalVelocity", "m/s"),
+                 ("GasTotalVelocityX", "m/s"), ("GasTotalVelocityY", "m/s"), ("GasTotalVelocityZ", "m/s"),
+                 ("GasTotalPhase", "1"), ("LiqTotalVelocity", "m/s"), ("LiqTotalVelocityX", "m/s"),
+                 ("LiqTotalVelocityY", "m/s"), ("LiqTotalVelocityZ", "m/s"), ("NumFluidCells", "1"),
+                 ("NumSpecialPoints", "1"), ("NumWallBoundaryPoints", "1"), ("NumBoundaryPoints", "1"),
+                 ("LiqTotalPhase", "1"), ("FluxNodeCount", "1"), ("FluxX", "1"), ("FluxY", "1"), ("FluxZ", "1")]:
+        m.add_global(g, unit=u)
+    m.options = {"q27": q27, "BGK": bgk, "OutFlow": False, "thermo": False, "planarBenchmark": False,
+                 "autosym": False, "geometric": False, "staircaseimp": False, "isograd": False, "tprec": False}
+    m.defines["hPops"] = str(Qh)
+    m.add_codegen(lambda _m: codegen(Qh))
+    m.set_dynamics("multiphase/d3q27_pf_velocity.inc")
+    return m
+
+
+def codegen(Qh: int) -> str:
+    M = moment_matrix()
+    Minv = M.inv()
+    P, Mraw = _raw_basis()
+    C = M * Mraw.inv()
+    Cinv = C.inv()
+    uu = sp.symbols("U V W")
+    p = sp.Symbol("p")
+    out = [f"  // ---- d3q27_pf_velocity moment algebra (model.R:16-46), M = C . Mraw"]
+    out.append(tensor_raw_transform("pf_raw", U27, P))
+    out.append(tensor_raw_transform("pf_rawinv", U27, P, inverse=True))
+    # low moments m0..m9 from raw moments (only these enter relaxation / stress)
+    out.append(dense_transform("pf_r2m_lo", C.T, 27, 10, "m[k<10] = C[k,:] . raw"))
+    out.append(dense_transform("pf_m2r", Cinv.T, 27, 27, "raw = C^-1 m"))
+    eq = mrt_eq(U27, rho=sp.Integer(1), J=uu, mat=M.T)
+    req = list(eq.Req)
+    req[0] = p
+    out.append(exprs_function("pf_req", ["p", "U", "V", "W"], req))
+    # stress of M^-1 m: s_ab = sum_i c_ia c_ib (M^-1 m)_i
+    pairs = [(0, 0), (0, 1), (0, 2), (1, 1), (1, 2), (2, 2)]
+    Srows = sp.Matrix([[sum(int(U27[i, a]) * int(U27[i, b]) * Minv[i, k] for i in range(27)) for k in range(27)]
+                       for a, b in pairs])
+    out.append(dense_transform("pf_stress", Srows.T, 27, 6, "stress = c c (M^-1 m)"))
+    Uh = U27[:Qh]
+    eqh = mrt_eq(Uh, rho=sp.Integer(1), J=uu)
+    out.append(exprs_function("pf_heq", ["U", "V", "W"], eqh.feq))
+    # ---- face boundary conditions (Boundary.c.Rt:31-108)
+    gs = [sp.Symbol(f"g_{i}") for i in range(27)]
+    hs = [sp.Symbol(f"h_{i}") for i in range(Qh)]
+    ren = {s: f"g[{i}]" for i, s in enumerate(gs)}
+    ren.update({s: f"h[{i}]" for i, s in enumerate(hs)})
+    bg = _bounce(U27)
+    bh = _bounce(Uh)
+    geq_vel = [sp.expand(e) for e in Minv * sp.Matrix(req)]   # feq with Req[0]=p (p cancels below)
+    feq1 = list(eq.feq)                                        # feq with Req[0]=1
+    w_g = [sp.nsimplify(e.subs({uu[0]: 0, uu[1]: 0, uu[2]: 0})) for e in feq1]
+    pstar = sp.Symbol("pstar")
+    pf = sp.Symbol("pf")
+    heq_bc = [pf * e for e in (eqh.feq if Qh == 27 else
+                               mrt_eq(Uh, rho=sp.Integer(1), J=(0, 0, 0)).feq)]
+    for name, n in FACES:
+        n = np.array(n)
+        # g, velocity type
+        cn = U27 @ n
+        sel = [i for i in range(27) if cn[i] < 0]
+        sel2 = [i for i in range(27) if cn[i] == 0]
+        exM = sp.Matrix([[sum((gs[i] - geq_vel[i]) * int(U27[i, d]) for i in sel2) for d in range(3)]])
+        Us = sp.Matrix(U27[sel].tolist())
+        Nmat = Us.T * Us
+        corr = exM * Nmat.inv() * sp.Matrix(U27.tolist()).T
+        exprs = [sp.expand(gs[bg[i]] + (geq_vel[i] - geq_vel[bg[i]]) - sp.Rational(1, 2) * corr[0, i]) for i in sel]
+        if any(sp.Symbol("p") in e.free_symbols for e in exprs):
+            raise AssertionError("pressure term must cancel in the velocity boundary condition")
+        out.append(f"  TCLB_FN void pf_bc_vel_g_{name}() {{")
+        out.append(assign_block([f"g[{i}]" for i in sel], exprs, rename=ren, tmp_prefix="b_"))
+        out.append("  }")
+        # g, pressure type
+        geq = [pstar * w_g[i] + (feq1[i] - w_g[i]) for i in range(27)]
+        exS = sum(gs[i] - geq[i] for i in sel2)
+        exprs = [sp.expand(geq[i] + geq[bg[i]] - gs[bg[i]] - sp.Rational(1, 2) * sp.Rational(1, len(sel)) * exS)
+                 for i in sel]
+        out.append(f"  TCLB_FN void pf_bc_press_g_{name}(R pstar) {{")
+        out.append(assign_block([f"g[{i}]" for i in sel], exprs, rename=ren, tmp_prefix="b_"))
+        out.append("  }")
+        # h (same for velocity and pressure type)
+        cn = Uh @ n
+        sel = [i for i in range(Qh) if cn[i] < 0]
+        sel2 = [i for i in range(Qh) if cn[i] == 0]
+        exS = sum(hs[i] - heq_bc[i] for i in sel2)
+        exprs = [sp.expand(heq_bc[i] + heq_bc[bh[i]] - hs[bh[i]] - sp.Rational(1, 2) * sp.Rational(1, len(sel)) * exS)
+                 for i in sel]
+        out.append(f"  TCLB_FN void pf_bc_h_{name}(R pf) {{")
+        out.append(assign_block([f"h[{i}]" for i in sel], exprs, rename=ren, tmp_prefix="b_"))
+        out.append("  }")
+    return "\n".join(out)

@@ -63,3 +63,6 @@ register("auto_part", ".flow.auto", part=True)
 register("auto_BGK", ".flow.auto", coll="BGK")
 register("auto_TRT", ".flow.auto", coll="TRT")
 register("d3q19_les", ".flow.d3q19_les")
+register("d3q27_pf_velocity", ".multiphase.d3q27_pf_velocity")
+register("d3q27_pf_velocity_q27", ".multiphase.d3q27_pf_velocity", q27=True)
+register("d3q27_pf_velocity_BGK", ".multiphase.d3q27_pf_velocity", bgk=True)

@@ -1,12 +1,34 @@
 #!/bin/bash
-# One GPU session: tests, benches, rocprof stats.  Every GPU step has its own timeout;
-# steps are chained with && so the first failure ends the call.
+# One GPU session: tests, benches, per-model table, rocprof stats.
+# Every GPU step has its own timeout; a crash/timeout (rc >= 124) ends the call, and
+# only an ordinary test failure (rc 1) lets the following steps run.
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out
 mkdir -p $O
 cd $R
-echo "== gpu tests" && timeout -k 10 600 python -m pytest tests -x -q -m gpu > $O/pytest_gpu.log 2>&1 ; tail -3 $O/pytest_gpu.log
-echo "== bench fp64" && timeout -k 10 300 python bench.py --steps 20 --warmup 3 > $O/bench_fp64.json 2> $O/bench_fp64.err && cat $O/bench_fp64.json &&
-echo "== bench fp32" && timeout -k 10 300 python bench.py --steps 20 --warmup 3 --precision float > $O/bench_fp32.json 2> $O/bench_fp32.err && cat $O/bench_fp32.json &&
-echo "== rocprof" && cd /tmp && export TMPDIR=/tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/prof -o run --output-format csv -- python3 $R/bench.py --steps 10 --warmup 2 > $O/prof.log 2>&1 ; echo "rocprof rc=$?"; ls -R $O/prof | head -20
+step() {  # step <name> <timeout> <logfile> cmd...
+  local name=$1 t=$2 log=$3; shift 3
+  echo "== $name"
+  timeout -k 10 $t "$@" > $log 2>&1
+  local rc=$?
+  tail -3 $log
+  echo "   rc=$rc"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
+  return 0
+}
+WHAT=${1:-all}
+if [ "$WHAT" = all ] || [ "$WHAT" = tests ]; then
+  step "gpu tests" 900 $O/pytest_gpu.log python -m pytest tests -x -q -m gpu
+fi
+if [ "$WHAT" = all ] || [ "$WHAT" = bench ]; then
+  step "bench fp64" 300 $O/bench_fp64.json python bench.py --steps 20 --warmup 3
+  step "bench fp32" 300 $O/bench_fp32.json python bench.py --steps 20 --warmup 3 --precision float
+fi
+if [ "$WHAT" = all ] || [ "$WHAT" = models ]; then
+  step "model table" 600 $O/perf_models_fp64.log python tools/perf_models.py
+fi
+if [ "$WHAT" = all ] || [ "$WHAT" = prof ]; then
+  cd /tmp && export TMPDIR=/tmp
+  step "rocprof" 400 $O/prof.log rocprofv3 --kernel-trace --stats -d $O/prof -o run --output-format csv -- python3 $R/bench.py --steps 10 --warmup 2
+fi
