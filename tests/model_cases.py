@@ -17,6 +17,22 @@ def collision_value(m):
     return 0
 
 
+# model-family settings for a physically meaningful small case (defaults of some models,
+# e.g. zero densities of the phase-field models, are not runnable as they stand)
+CASE_SETTINGS = {
+    "d3q27_pf_velocity": {"Density_h": 1.0, "Density_l": 0.1, "sigma": 1e-3, "Viscosity_l": 0.05,
+                          "Viscosity_h": 0.05, "M": 0.05, "PhaseField": 1.0, "Radius": 4.0,
+                          "CenterX": 12.0, "CenterY": 6.0, "CenterZ": 5.0, "BubbleType": -1.0},
+}
+
+
+def case_settings(name):
+    for k, v in CASE_SETTINGS.items():
+        if name == k or name.startswith(k + "_"):
+            return v
+    return {}
+
+
 def make_case(name, device="cpu", precision="double", shape=None, comm=None):
     m = registry.get(name)
     shape = shape or (SMALL_2D if m.dims == 2 else SMALL_3D)
@@ -27,6 +43,8 @@ def make_case(name, device="cpu", precision="double", shape=None, comm=None):
     if wall is not None:
         fl[:, :, 0] = wall.value   # x = 0 plane of walls (not on the decomposed axis)
     lat.set_flags(fl)
+    for k, v in case_settings(name).items():
+        lat.set_setting(k, v)
     return lat
 
 

@@ -1,0 +1,117 @@
+#!/usr/bin/env python3
+"""Single-GPU throughput of the secondary BASELINE.json configurations (bench.py is the
+headline d3q27 512^3 metric).  One JSON line per config:
+
+  cavity  d3q19 BGK lid-driven cavity 256^3   (auto_d3q19_BGK: walls on 5 faces, ZouHe
+          velocity lid on y = ny-1)
+  pf384   d3q27 two-distribution multiphase droplet 384^3 (d3q27_pf_velocity: g D3Q27 +
+          h D3Q15, 4-stage Iteration action, density ratio 10)
+  part256 d3q19 + moving particle 256^3 (auto_d3q19_part: BaseIteration + particle CalcF
+          stage, one sphere integrated in-process)
+
+MLUPS = nodes x steps / wall time of the timed window (all stages, halos, globals on the
+last step), the reference meter's definition (src/main.cpp:101-127).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from tclb_amd.lattice import Lattice  # noqa: E402
+
+
+def _time(lat, steps, warmup):
+    lat.iterate(warmup, glob_last=False)
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    lat.iterate(steps, glob_last=True)
+    torch.cuda.synchronize()
+    return time.perf_counter() - t
+
+
+def cavity(n, precision, dev):
+    lat = Lattice("auto_d3q19_BGK", (n, n, n), device=dev, precision=precision)
+    m = lat.model
+    fl = np.full((lat.NZ, lat.NY, n), m.node_type("MRT").value, dtype=np.uint32)
+    wall = m.node_type("Wall").value
+    gz, gy = lat.gz, lat.gy
+    fl[:, gy + 0, :] = wall
+    fl[:, :, 0] = wall
+    fl[:, :, n - 1] = wall
+    fl[gz + 0, :, :] = wall
+    fl[gz + n - 1, :, :] = wall
+    fl[gz + 1:gz + n - 1, gy + n - 1, 1:n - 1] = m.node_type("NVelocity").value | m.node_type("MRT").value
+    lat.set_flags(fl)
+    lat.set_setting("Viscosity", 0.01)
+    lat.set_setting("Velocity", 0.05)
+    lat.init()
+    return lat
+
+
+def pf384(n, precision, dev):
+    lat = Lattice("d3q27_pf_velocity", (n, n, n), device=dev, precision=precision)
+    fl = np.full((lat.NZ, lat.NY, n), lat.model.node_type("MRT").value, dtype=np.uint32)
+    lat.set_flags(fl)
+    for k, v in {"Density_h": 1.0, "Density_l": 0.1, "sigma": 0.01, "Viscosity_l": 0.1, "Viscosity_h": 0.1,
+                 "M": 0.05, "BubbleType": 1.0, "IntWidth": 4.0, "Radius": n / 4,
+                 "CenterX": n / 2, "CenterY": n / 2, "CenterZ": n / 2}.items():
+        lat.set_setting(k, v)
+    lat.init()
+    return lat
+
+
+def part256(n, precision, dev):
+    from tclb_amd.particles import SimplePart
+    lat = Lattice("auto_d3q19_part", (n, n, n), device=dev, precision=precision)
+    m = lat.model
+    fl = np.full((lat.NZ, lat.NY, n), m.node_type("MRT").value, dtype=np.uint32)
+    lat.set_flags(fl)
+    lat.set_setting("Viscosity", 0.05)
+    lat.set_setting("ForceX", 1e-6)
+    ps = SimplePart()
+    ps.add(x=(n / 2, n / 2, n / 2), r=n / 16, v=(0.01, 0, 0), m=1e4)
+    ps.periodic[:] = True
+    ps.period[:] = n
+    lat.particles = ps
+    lat.init()
+    return lat
+
+
+CONFIGS = {"cavity": (cavity, 256, "d3q19 BGK lid-driven cavity 256^3"),
+           "pf384": (pf384, 384, "d3q27 multiphase droplet 384^3 (two distribution sets)"),
+           "part256": (part256, 256, "d3q19 + moving particle 256^3")}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--configs", default="cavity,pf384,part256")
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--precision", default="double")
+    ap.add_argument("--size", type=int, default=0, help="override lattice size")
+    a = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    for name in a.configs.split(","):
+        fn, n, desc = CONFIGS[name]
+        n = a.size or n
+        lat = fn(n, a.precision, dev)
+        dt = _time(lat, a.steps, a.warmup)
+        nodes = n ** 3
+        out = {"config": name, "desc": desc, "model": lat.model.name, "lattice": [n, n, n],
+               "precision": a.precision, "steps": a.steps, "ms_per_step": round(dt / a.steps * 1e3, 4),
+               "MLUPS": round(nodes * a.steps / dt / 1e6, 1),
+               "fields": lat.nf, "stages": len(lat.model.action("Iteration").stages),
+               "globals_finite": bool(all(np.isfinite(v) for v in lat.globals.values())),
+               "memory_GB": round(lat.memory_bytes() / 1e9, 2)}
+        print(json.dumps(out), flush=True)
+        del lat
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()
