@@ -140,12 +140,13 @@ TCLB_FN void zouhe(R* f, bool pressure, R value, R& rho_out, R* J, const R* vt =
   TCLB_UNROLL for (int t = 0; t < L::D; t++) {
     if (t == AX) continue;
     const double T = zh_T<L>(AX, SGN, t);
-    if (MODE == ZH_REF) J[t] = B[t] * R(1.0 / (1.0 - T));
-    else J[t] = -B[t] * R(1.0 / T);
-  }
-  if (vt != nullptr) {
-    TCLB_UNROLL for (int t = 0; t < L::D; t++)
-      if (t != AX) J[t] += rho * vt[t];
+    if (MODE == ZH_REF) {
+      J[t] = B[t] * R(1.0 / (1.0 - T));
+      if (vt != nullptr) J[t] += rho * vt[t];
+    } else {
+      // ZouHeRewrite: sum fs c_t = rho vt_t  ->  J_t = (rho vt_t - B_t) / T_t
+      J[t] = ((vt != nullptr ? rho * vt[t] : R(0)) - B[t]) * R(1.0 / T);
+    }
   }
   if (L::D < 3) J[2] = R(0);
   if (L::D < 2) J[1] = R(0);

@@ -290,6 +290,12 @@ class Model:
             self.add_setting(f"{g.name}InObj", default=0.0, zonal=True,
                              comment=f"Weight of [{g.comment or g.name}] in objective", preload=False)
         self.add_setting("Threshold", default=0.5, comment="Parameters threshold")
+        autosym = int(self.options.get("autosym", 0) or 0)
+        if autosym:   # automatic symmetry node types (src/conf.R:440-457)
+            nm = "Symmetry" if autosym == 1 else "SymmetryEdge"
+            for ax in ("X", "Y", "Z")[:max(2, self.dims)]:
+                self.add_node_type(f"{nm}{ax}_plus", f"SYM{ax}")
+                self.add_node_type(f"{nm}{ax}_minus", f"SYM{ax}")
         self._pack_node_types()
         self._check_stage_access()
         self._finalized = True

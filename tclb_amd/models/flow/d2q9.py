@@ -1,6 +1,7 @@
 """d2q9 — weighted-orthogonal MRT with Zou/He (rewrite form) velocity/pressure
 boundaries, symmetry and bounce-back; objective globals on Inlet/Outlet nodes.
-Reference: models/flow/d2q9/Dynamics.R, Dynamics.c.Rt (base variant, no bc/autosym)."""
+Reference: models/flow/d2q9/Dynamics.R, Dynamics.c.Rt (OPT="bc*autosym": variants
+d2q9, d2q9_bc, d2q9_autosym, d2q9_bc_autosym)."""
 import numpy as np
 import sympy as sp
 
@@ -32,12 +33,15 @@ def d2q9_mrt_basis():
     return B
 
 
-def build(bc: bool = False) -> Model:
+def build(bc: bool = False, autosym: int = 0) -> Model:
     m = Model("d2q9", dims=2, family="flow", reference="models/flow/d2q9",
               description="D2Q9 MRT (weighted orthogonal basis) with Zou/He and symmetry boundaries")
     shifts = [4 / 9] + [1 / 9] * 4 + [1 / 36] * 4
     for i, (x, y) in enumerate(U9):
         m.add_density(f"f[{i}]", int(x), int(y), 0, group="f", shift=shifts[i])
+    if bc:
+        m.add_density("BC[0]", group="BC", parameter=True)
+        m.add_density("BC[1]", group="BC", parameter=True)
     m.add_quantity("Rho", unit="kg/m3")
     m.add_quantity("U", unit="m/s", vector=True)
     m.add_setting("RelaxationRate", comment="one over relaxation time", S2="1-RelaxationRate")
@@ -60,7 +64,7 @@ def build(bc: bool = False) -> Model:
     m.add_node_type("Solid", "BOUNDARY")
     m.add_node_type("Wall", "BOUNDARY")
     m.add_node_type("MRT", "COLLISION")
-    m.options = {"bc": bc, "autosym": False}
+    m.options = {"bc": bc, "autosym": autosym}
     B = d2q9_mrt_basis()
     eq = mrt_eq(U9, mat=B)
     m.add_codegen(lambda _m: mrt_block("mrt", eq))

@@ -66,3 +66,7 @@ register("d3q19_les", ".flow.d3q19_les")
 register("d3q27_pf_velocity", ".multiphase.d3q27_pf_velocity")
 register("d3q27_pf_velocity_q27", ".multiphase.d3q27_pf_velocity", q27=True)
 register("d3q27_pf_velocity_BGK", ".multiphase.d3q27_pf_velocity", bgk=True)
+register("d2q9_bc", ".flow.d2q9", bc=True)
+register("d2q9_autosym", ".flow.d2q9", autosym=1)
+register("d2q9_bc_autosym", ".flow.d2q9", bc=True, autosym=1)
+register("d2q9_kuper", ".multiphase.d2q9_kuper")

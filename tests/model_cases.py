@@ -20,6 +20,8 @@ def collision_value(m):
 # model-family settings for a physically meaningful small case (defaults of some models,
 # e.g. zero densities of the phase-field models, are not runnable as they stand)
 CASE_SETTINGS = {
+    "d2q9_kuper": {"Density": 1.0, "Temperature": 0.65, "Magic": 0.005, "FAcc": 1.0, "nu": 0.1666},
+    "d3q19_kuper": {"Density": 1.0, "Temperature": 0.65, "Magic": 0.005, "FAcc": 1.0, "nu": 0.1666},
     "d3q27_pf_velocity": {"Density_h": 1.0, "Density_l": 0.1, "sigma": 1e-3, "Viscosity_l": 0.05,
                           "Viscosity_h": 0.05, "M": 0.05, "PhaseField": 1.0, "Radius": 4.0,
                           "CenterX": 12.0, "CenterY": 6.0, "CenterZ": 5.0, "BubbleType": -1.0},
