@@ -70,3 +70,6 @@ register("d2q9_bc", ".flow.d2q9", bc=True)
 register("d2q9_autosym", ".flow.d2q9", autosym=1)
 register("d2q9_bc_autosym", ".flow.d2q9", bc=True, autosym=1)
 register("d2q9_kuper", ".multiphase.d2q9_kuper")
+register("d2q9_pf", ".multiphase.d2q9_pf")
+register("d2q9_pf_no_bc", ".multiphase.d2q9_pf", no_bc=True)
+register("d2q9_pf_fd", ".multiphase.d2q9_pf", fd=True)

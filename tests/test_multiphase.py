@@ -71,3 +71,31 @@ def test_kuper_coexistence():
     assert abs(r[2, 2] - 0.065) < 0.01
     assert abs(r.sum() / m0 - 1) < 1e-11
     assert np.abs(lat.quantity("U").numpy()).max() < 5e-3
+
+
+@pytest.mark.parametrize("name", ["d2q9_pf", "d2q9_pf_fd"])
+def test_phase_field_profile(name):
+    """d2q9_pf (reference models/multiphase/d2q9_pf): a slab of phase +1/2 in -1/2
+    relaxes to the conservative Allen-Cahn equilibrium profile 1/2 tanh(2 W x)
+    (W = IntWidth), with the phase field conserved."""
+    import torch
+    from tclb_amd.lattice import Lattice
+    n, W = 64, 0.25
+    lat = Lattice(name, (n, 4, 1), device=torch.device("cpu"), precision="double")
+    m = lat.model
+    zi = lat.add_zone("liq")
+    fl = np.full((lat.NZ, lat.NY, n), m.node_type("MRT").value, dtype=np.uint32)
+    fl[:, :, 16:48] |= (zi << m.zone_shift)
+    lat.set_flags(fl)
+    for k, v in {"IntWidth": W, "Mobility": 0.05, "Viscosity": 0.1}.items():
+        lat.set_setting(k, v)
+    lat.set_setting("PhaseField", -0.5)
+    lat.set_setting("PhaseField", 0.5, zone="liq")
+    lat.init()
+    p0 = (lat.quantity("PhaseField").numpy() + 0.5).sum()
+    lat.iterate(3000)
+    p = lat.quantity("PhaseField").numpy()[0, 0]
+    x = np.arange(n) + 0.0
+    ref = np.where(x < 32, 0.5 * np.tanh(2 * W * (x - 15.5)), -0.5 * np.tanh(2 * W * (x - 47.5)))
+    assert np.abs(p - ref[None]).max() < 0.01
+    assert abs((p + 0.5).sum() / p0 - 1) < 1e-12
