@@ -20,6 +20,8 @@ def collision_value(m):
 # model-family settings for a physically meaningful small case (defaults of some models,
 # e.g. zero densities of the phase-field models, are not runnable as they stand)
 CASE_SETTINGS = {
+    "d2q9_npe_guo": {"epsilon": 50.0, "nu": 0.1, "n_inf_0": 1.0, "n_inf_1": 1.0, "el": 1.0, "el_kbT": 1.0,
+                     "psi_bc": 0.01},
     "d2q9_kuper": {"Density": 1.0, "Temperature": 0.65, "Magic": 0.005, "FAcc": 1.0, "nu": 0.1666},
     "d3q19_kuper": {"Density": 1.0, "Temperature": 0.65, "Magic": 0.005, "FAcc": 1.0, "nu": 0.1666},
     "d3q27_pf_velocity": {"Density_h": 1.0, "Density_l": 0.1, "sigma": 1e-3, "Viscosity_l": 0.05,
