@@ -74,3 +74,4 @@ register("d2q9_pf", ".multiphase.d2q9_pf")
 register("d2q9_pf_no_bc", ".multiphase.d2q9_pf", no_bc=True)
 register("d2q9_pf_fd", ".multiphase.d2q9_pf", fd=True)
 register("d2q9_npe_guo", ".electrokinetic.d2q9_npe_guo")
+register("d2q9_thin_film", ".flow.d2q9_thin_film")
