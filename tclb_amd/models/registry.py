@@ -75,3 +75,10 @@ register("d2q9_pf_no_bc", ".multiphase.d2q9_pf", no_bc=True)
 register("d2q9_pf_fd", ".multiphase.d2q9_pf", fd=True)
 register("d2q9_npe_guo", ".electrokinetic.d2q9_npe_guo")
 register("d2q9_thin_film", ".flow.d2q9_thin_film")
+register("d3q27_PSM", ".particles.d3q27_psm")
+register("d3q27_PSM_NEBB", ".particles.d3q27_psm", nebb=True)
+register("d3q27_PSM_SUP", ".particles.d3q27_psm", sup=True)
+register("d3q27_PSM_TRT_NEBB", ".particles.d3q27_psm", trt=True, nebb=True)
+register("d3q27_PSM_MS_NEBB", ".particles.d3q27_psm", ms=True, nebb=True)
+register("d3q27_PSM_KL_NEBB", ".particles.d3q27_psm", kl=True, nebb=True)
+register("d3q27_PSM_NEBB_singlekernel", ".particles.d3q27_psm", nebb=True, singlekernel=True)

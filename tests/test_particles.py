@@ -38,3 +38,31 @@ def test_sphere_drag_gpu_matches_cpu():
     b.iterate(10)
     assert np.allclose(pa.force, pb.force, rtol=1e-9, atol=1e-12)
     assert torch.allclose(a.fields_interior().cpu(), b.fields_interior(), atol=1e-12)
+
+
+@pytest.mark.parametrize("name", ["d3q27_PSM_NEBB", "d3q27_PSM_SUP", "d3q27_PSM_TRT_NEBB", "d3q27_PSM_MS_NEBB"])
+def test_psm_momentum_balance(name):
+    """d3q27_PSM (reference models/particles/d3q27_PSM): a fixed sphere in a periodic box
+    of fluid driven by a body acceleration; at steady state the hydrodynamic force on the
+    sphere balances the momentum injected into the domain, the solid
+    fraction integrates to ~ the sphere volume, and mass is conserved."""
+    n, a = 16, 1e-6
+    lat = Lattice(name, (n, n, n), device=torch.device("cpu"))
+    lat.set_flags(np.full((lat.NZ, lat.NY, n), lat.model.node_type("BGK").value, dtype=np.uint32))
+    lat.set_setting("nu", 0.3)
+    if "TRT" in name:
+        lat.set_setting("Lambda", 3 / 16)
+    lat.set_setting("aX_mean", a)
+    sp = SimplePart()
+    sp.add([8.0, 8.0, 8.0], 3.0, fixed=True)
+    lat.particles = sp
+    lat.init()
+    lat.iterate(3000)
+    sol = lat.quantity("Solid").numpy()[0]
+    rho = lat.quantity("Rho").numpy()[0]
+    injected = rho.sum() * a          # body force acts on every node (fluid and solid parts)
+    tol = 0.03 if "SUP" in name else 0.01    # superposition is not exactly momentum-conserving
+    assert abs(sp.force[0, 0] / injected - 1) < tol
+    assert abs(sp.force[0, 1]) < 1e-8 * injected and abs(sp.force[0, 2]) < 1e-8 * injected
+    assert abs(sol.sum() / (4 / 3 * np.pi * 27) - 1) < 0.25
+    assert abs(lat.globals["TotalFluidMass"] / n ** 3 - 1) < 1e-12
