@@ -38,6 +38,10 @@ class Solver:
                  precision: str = "double", comm: Optional[Comm] = None, block=(0, 0)):
         self.model_name = model
         self.model = registry.get(model)
+        from .utils.xpath import rewrite_deprecated_params
+        n = rewrite_deprecated_params(config)
+        if n:
+            log.warning(f"{n} deprecated Params elements found. Changing them to Param")
         self.config_tree = config
         self.conffile = conffile
         self.comm = comm or LoopbackComm()

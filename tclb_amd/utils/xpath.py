@@ -128,3 +128,36 @@ def apply_edits(root: ET.Element, argv: List[str]) -> Tuple[ET.Element, bool]:
 
 def strip_comments(root: ET.Element) -> ET.Element:
     return root  # ElementTree drops comments by default
+
+
+def rewrite_deprecated_params(root):
+    """<Params a="1" b-zone="2" gauge="g"/> -> one <Param name= value= [zone=] [gauge=]/>
+    per attribute, in place, and switch the config to permissive mode (reference
+    src/main.cpp:261-293).  Returns the number of rewritten elements."""
+    count = 0
+    for parent in list(root.iter()):
+        kids = list(parent)
+        for node in kids:
+            if node.tag != "Params":
+                continue
+            count += 1
+            gauge = node.get("gauge")
+            pos = list(parent).index(node)
+            new = []
+            for k, v in node.attrib.items():
+                if k == "gauge":
+                    continue
+                par, _, zone = k.partition("-")
+                p = ET.Element("Param", {"name": par, "value": v})
+                if zone:
+                    p.set("zone", zone)
+                if gauge is not None:
+                    p.set("gauge", gauge)
+                p.tail = node.tail
+                new.append(p)
+            parent.remove(node)
+            for j, p in enumerate(new):
+                parent.insert(pos + j, p)
+    if count:
+        root.set("permissive", "true")
+    return count

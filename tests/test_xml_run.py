@@ -97,3 +97,19 @@ def test_cli_module(tmp_path):
                        capture_output=True, text=True, env={**os.environ, "PYTHONPATH": os.getcwd() + ":" +
                                                             os.path.dirname(os.path.dirname(os.path.abspath(__file__)))})
     assert r.returncode == 0, r.stderr
+
+
+def test_deprecated_params_rewrite():
+    """<Params a=.. b-zone=.. gauge=..> becomes one <Param> per attribute and the run
+    turns permissive (reference src/main.cpp:261-293)."""
+    import xml.etree.ElementTree as ET
+    from tclb_amd.utils.xpath import rewrite_deprecated_params
+    root = ET.fromstring('<CLBConfig><Units><Params x="8um" gauge="64"/></Units>'
+                         '<Model><Params nu="0.1" psi_bc-wall="0.025V"/><Param name="k" value="1"/></Model></CLBConfig>')
+    assert rewrite_deprecated_params(root) == 2
+    assert root.get("permissive") == "true"
+    u = root.find("Units/Param")
+    assert (u.get("name"), u.get("value"), u.get("gauge")) == ("x", "8um", "64")
+    ps = root.findall("Model/Param")
+    assert [(p.get("name"), p.get("value"), p.get("zone")) for p in ps] == [
+        ("nu", "0.1", None), ("psi_bc", "0.025V", "wall"), ("k", "1", None)]
