@@ -130,10 +130,46 @@ def build_host(force: bool = False, verbose: bool = False) -> str:
     return target
 
 
+BIN = os.path.join(BUILD, "bin")
+
+
+def tool_path(name: str) -> str:
+    return os.path.join(BIN, f"tclb-{name}")
+
+
+def build_tools(force: bool = False, verbose: bool = False) -> Dict[str, str]:
+    """native auxiliary executables (reference src/compare.cpp etc.): csrc/tools/<name>.cpp
+    -> _build/bin/tclb-<name>"""
+    tdir = os.path.join(CSRC, "tools")
+    os.makedirs(BIN, exist_ok=True)
+    out = {}
+    for fn in sorted(os.listdir(tdir)):
+        if not fn.endswith(".cpp"):
+            continue
+        name = fn[:-4]
+        src = os.path.join(tdir, fn)
+        target = tool_path(name)
+        cmd = [CXX, "-O2", "-std=c++17", "-fopenmp", src, "-o", target + ".tmp"]
+        h = _hash_inputs([src], " ".join(cmd))
+        stamp = target + ".hash"
+        if force or not (os.path.exists(target) and os.path.exists(stamp) and open(stamp).read() == h):
+            r = subprocess.run(cmd, capture_output=True, text=True)
+            if r.returncode != 0:
+                raise RuntimeError(f"tool {name} build failed:\n{r.stderr[-10000:]}")
+            os.replace(target + ".tmp", target)
+            with open(stamp, "w") as f:
+                f.write(h)
+            if verbose:
+                print(f"[tclb build] tool tclb-{name}", flush=True)
+        out[name] = target
+    return out
+
+
 def build_all(models: Optional[List[str]] = None, kinds=("cpu", "hip"), jobs: int = 0, force=False,
               verbose=False) -> Dict[str, Dict[str, str]]:
     models = models or registry.names()
     build_host(force=force, verbose=verbose)
+    build_tools(force=force, verbose=verbose)
     jobs = jobs or max(1, min(8, os.cpu_count() or 1))
     tasks = [(m, k) for m in models for k in kinds]
     res: Dict[str, Dict[str, str]] = {m: {} for m in models}

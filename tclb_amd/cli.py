@@ -24,7 +24,7 @@ def main(argv=None):
     ap.add_argument("--precision", default="double", choices=["double", "float", "mixed"])
     ap.add_argument("--list", action="store_true")
     ap.add_argument("--describe", action="store_true")
-    a = ap.parse_args(argv)
+    a = ap.parse_intermixed_args(argv)   # options may follow the model / case file
     from .models import registry
     if a.list or a.model == "list":
         print("\n".join(registry.names()))
