@@ -169,7 +169,9 @@ TCLB_FN void particle_flush(double* acc, const ParticleS<R>& p) {
   double* a = acc + (long long)p.i * 6;
 #if TCLB_GPU && defined(__HIP_DEVICE_COMPILE__)
   const unsigned long long act = __ballot(1);
-  if (act == ~0ull) {
+  // wave reduction only when every lane is active on the same particle (grid candidate
+  // lists differ between lanes of different cells)
+  if (act == ~0ull && __all(p.i == __shfl(p.i, 0, 64))) {
     const int lane = __lane_id();
     TCLB_UNROLL for (int k = 0; k < 6; k++) {
       double s = v[k];

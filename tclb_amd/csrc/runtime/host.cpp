@@ -156,5 +156,41 @@ long long tclb_nan_scan_f32(const float* a, long long n) {
   return bad;
 }
 
-int tclb_host_version() { return 1; }
+// Uniform-grid solid container (reference SolidGrid, src/SolidGrid.h:16-179): particles
+// binned by centre into cubic cells of edge `cell` (>= max radius + interaction range)
+// covering the lattice [0,nx)x[0,ny)x[0,nz); centres outside are clamped into the border
+// cells.  Output layout (int32), read by the device ParticleLoop:
+//   [0..7]  gx, gy, gz, cell, 0, 0, 0, 0
+//   [8 .. 8+ncell]          CSR start of every cell (ncell+1 entries)
+//   [9+ncell .. 9+ncell+n)  particle indices sorted by cell
+// Returns the number of ints written, or -1 if `cap` is too small.
+long long tclb_solid_grid(const double* P, int n, int stride, int nx, int ny, int nz, int cell, int* out,
+                          long long cap) {
+  if (cell < 1) cell = 1;
+  const int gx = (nx + cell - 1) / cell, gy = (ny + cell - 1) / cell, gz = (nz + cell - 1) / cell;
+  const long long ncell = (long long)gx * gy * gz;
+  const long long need = 8 + ncell + 1 + n;
+  if (need > cap) return -1;
+  out[0] = gx; out[1] = gy; out[2] = gz; out[3] = cell;
+  out[4] = out[5] = out[6] = out[7] = 0;
+  int* start = out + 8;
+  int* ids = out + 9 + ncell;
+  std::vector<int> cid(n);
+  for (long long c = 0; c <= ncell; c++) start[c] = 0;
+  auto clampi = [](long long v, int hi) { return (int)(v < 0 ? 0 : (v >= hi ? hi - 1 : v)); };
+  for (int i = 0; i < n; i++) {
+    const double* p = P + (size_t)i * stride;
+    const int cx = clampi((long long)std::floor(p[0] / cell), gx);
+    const int cy = clampi((long long)std::floor(p[1] / cell), gy);
+    const int cz = clampi((long long)std::floor(p[2] / cell), gz);
+    cid[i] = (int)(((long long)cz * gy + cy) * gx + cx);
+    start[cid[i] + 1]++;
+  }
+  for (long long c = 0; c < ncell; c++) start[c + 1] += start[c];
+  std::vector<int> fill(start, start + ncell);
+  for (int i = 0; i < n; i++) ids[fill[cid[i]]++] = i;
+  return need;
+}
+
+int tclb_host_version() { return 2; }
 }

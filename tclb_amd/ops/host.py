@@ -26,6 +26,8 @@ def lib():
             L.tclb_stl_fill.restype = ctypes.c_longlong
             L.tclb_stl_cuts.argtypes = [P, i, i, i, i, i, i, i, P, P, P]
             L.tclb_stl_cuts.restype = ctypes.c_longlong
+            L.tclb_solid_grid.argtypes = [P, i, i, i, i, i, i, P, ctypes.c_longlong]
+            L.tclb_solid_grid.restype = ctypes.c_longlong
             L.tclb_nan_scan_f64.argtypes = [P, ctypes.c_longlong]
             L.tclb_nan_scan_f64.restype = ctypes.c_longlong
             L.tclb_nan_scan_f32.argtypes = [P, ctypes.c_longlong]
@@ -60,3 +62,18 @@ def nan_count(a: np.ndarray) -> int:
     if a.dtype == np.float32:
         return int(lib().tclb_nan_scan_f32(a.ctypes.data, a.size))
     return int((~np.isfinite(a)).sum())
+
+
+def solid_grid(rec: np.ndarray, shape, cell: int) -> np.ndarray:
+    """uniform-grid solid container of particle records (n, stride) over a lattice of
+    global shape (nx, ny, nz); see tclb_solid_grid in csrc/runtime/host.cpp"""
+    rec = np.ascontiguousarray(rec, dtype=np.float64)
+    n, stride = rec.shape
+    nx, ny, nz = shape
+    cell = max(1, int(cell))
+    ncell = -(-nx // cell) * -(-ny // cell) * -(-nz // cell)
+    out = np.zeros(9 + ncell + n, dtype=np.int32)
+    r = lib().tclb_solid_grid(rec.ctypes.data, n, stride, nx, ny, nz, cell, out.ctypes.data, out.size)
+    if r < 0:
+        raise RuntimeError("solid grid buffer too small")
+    return out[:r]

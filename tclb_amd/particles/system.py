@@ -25,6 +25,8 @@ class ParticleSystem:
         self.fixed = np.zeros(n, dtype=bool)
         self._dev = None
         self._acc = None
+        self._grid = None
+        self.grid_min = 16          # particles; below this every node scans the full list
 
     @property
     def n(self) -> int:
@@ -54,6 +56,19 @@ class ParticleSystem:
         L.ext[2] = self._dev.data_ptr()
         L.ext[3] = self._acc.data_ptr()
         L.next[2] = self.n
+        # solid container: uniform grid (reference default SolidGrid) once the linear scan
+        # over all particles per node stops being cheap
+        self._grid = None
+        if self.n >= self.grid_min:
+            from ..ops.host import solid_grid
+            cell = int(np.ceil(self.r[:self.n].max() + 2.0)) if self.n else 1
+            g = solid_grid(rec[:self.n], lat.gshape, cell)
+            self._grid = torch.as_tensor(g).to(lat.device)
+            L.ext[4] = self._grid.data_ptr()
+            L.next[4] = self._grid.numel()
+        else:
+            L.ext[4] = None
+            L.next[4] = 0
 
     def post_stage(self, lat):
         acc = self._acc
@@ -63,6 +78,8 @@ class ParticleSystem:
         self.force = a[:, 0:3].copy()
         self.torque = a[:, 3:6].copy()
         lat._L.next[2] = 0
+        lat._L.ext[4] = None
+        lat._L.next[4] = 0
 
     def step(self, lat):
         """advance after the particle stage of one iteration"""

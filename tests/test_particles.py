@@ -66,3 +66,38 @@ def test_psm_momentum_balance(name):
     assert abs(sp.force[0, 1]) < 1e-8 * injected and abs(sp.force[0, 2]) < 1e-8 * injected
     assert abs(sol.sum() / (4 / 3 * np.pi * 27) - 1) < 0.25
     assert abs(lat.globals["TotalFluidMass"] / n ** 3 - 1) < 1e-12
+
+
+def _many(device, grid_min, n=24, count=30):
+    lat = Lattice("d3q27_PSM_NEBB", (n, n, n), device=torch.device(device))
+    lat.set_flags(np.full((lat.NZ, lat.NY, n), lat.model.node_type("BGK").value, dtype=np.uint32))
+    lat.set_setting("nu", 0.1)
+    lat.set_setting("aX_mean", 1e-5)
+    sp = SimplePart()
+    sp.grid_min = grid_min
+    rng = np.random.default_rng(1)
+    for _ in range(count):
+        sp.add(rng.uniform(-2, n + 2, 3), rng.uniform(1, 2.5), v=rng.uniform(-0.01, 0.01, 3),
+               omega=rng.uniform(-0.01, 0.01, 3), fixed=True)
+    lat.particles = sp
+    lat.init()
+    lat.iterate(4)
+    return lat.fields_interior().cpu(), sp.force.copy(), sp.torque.copy()
+
+
+def test_solid_grid_matches_linear_scan():
+    """uniform-grid solid container (reference SolidGrid) gives the same coupling as
+    scanning every particle at every node (reference SolidAll / tests/solid)."""
+    fa, Fa, Ta = _many("cpu", 10 ** 9)
+    fb, Fb, Tb = _many("cpu", 1)
+    assert torch.equal(fa, fb)
+    assert np.allclose(Fa, Fb, rtol=1e-12, atol=1e-15) and np.allclose(Ta, Tb, rtol=1e-12, atol=1e-15)
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not torch.cuda.is_available(), reason="no GPU")
+def test_solid_grid_gpu_matches_cpu():
+    fa, Fa, Ta = _many("cuda", 1)
+    fb, Fb, Tb = _many("cpu", 10 ** 9)
+    assert torch.allclose(fa, fb, atol=1e-12)
+    assert np.allclose(Fa, Fb, rtol=1e-9, atol=1e-13) and np.allclose(Ta, Tb, rtol=1e-9, atol=1e-13)
