@@ -18,6 +18,7 @@ src/Lattice.cu.Rt).  Differences by design:
 from __future__ import annotations
 
 import math
+import os
 from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
@@ -83,10 +84,15 @@ class Lattice:
         self.rdtype = torch.float32 if precision == "float" else torch.float64
         nf = len(m.fields)
         self.nf = nf
-        self.fs = self.NZ * self.NY * self.px
+        plane = self.NZ * self.NY * self.px
+        # optional padding between field planes (elements, env TCLB_FIELD_PAD): staggers
+        # the 2 x nf concurrent HBM streams across channels; 0 = dense
+        self.field_pad = int(os.environ.get("TCLB_FIELD_PAD", "0"))
+        self.fs = plane + self.field_pad
         if self.fs >= 2 ** 31:
             raise ValueError("local field exceeds 2^31 elements; use more ranks")
-        self.snaps = [torch.zeros((nf, self.NZ, self.NY, self.px), dtype=self.sdtype, device=self.device)
+        self.snaps = [torch.zeros(nf * self.fs, dtype=self.sdtype, device=self.device)
+                      .as_strided((nf, self.NZ, self.NY, self.px), (self.fs, self.NY * self.px, self.px, 1))
                       for _ in range(2)]
         self.cur = 0
         fdt = torch.int16 if m.flag_bits == 16 else torch.int32
