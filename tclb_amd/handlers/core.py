@@ -242,6 +242,50 @@ class VTK(Callback):
         return self.solver.write_vtk(self.name, self.what, self.reg)
 
 
+@register("HDF5")
+class HDF5(Callback):
+    """reference cbHDF5 (src/Handlers/cbHDF5.cpp): region-cropped field output with an
+    XDMF sidecar.  libhdf5/h5py are not part of this image, so the data go to one raw
+    binary file per step that the .xmf describes (readable by ParaView/VisIt);
+    ``compress`` / ``chunk`` / ``point_data`` are accepted and ignored with a notice."""
+
+    def init(self):
+        super().init()
+        self.name = self.node.get("name", "HDF5")
+        self.what = _what(self.node)
+        self.reg = _region_attrs(self, self.solver.total)
+        if self.reg[3] * self.reg[4] * self.reg[5] == 0:
+            raise HandlerError(f'HDF5 "{self.name}" output has size 0')
+        prec = self.node.get("precision")
+        calc_double = self.solver.lattice.rdtype.itemsize == 8 if self.solver.lattice else True
+        self.double = calc_double if prec is None else prec == "double"
+        if prec not in (None, "double", "float"):
+            raise HandlerError("HDF5 precision should be double or float")
+        for a in ("compress", "chunk", "point_data"):
+            if self.node.get(a) is not None:
+                log.notice(f"HDF5: attribute {a} has no effect with the XDMF+binary container")
+        return 0
+
+    def do_it(self):
+        return self.solver.write_xdmf(self.name, self.what, self.reg, double=self.double)
+
+
+@register("Catalyst")
+class Catalyst(Callback):
+    """reference cbCatalyst (ParaView in-situ).  ParaView Catalyst is not available in this
+    image: the element is accepted, and every ``Iterations`` step falls back to writing a
+    VTK dataset that a Catalyst script could post-process offline."""
+
+    def init(self):
+        super().init()
+        log.warning("Catalyst: ParaView Catalyst not available; writing VTK output instead")
+        self.reg = _region_attrs(self, self.solver.total)
+        return 0
+
+    def do_it(self):
+        return self.solver.write_vtk(self.node.get("name", "Catalyst"), ["all"], self.reg)
+
+
 @register("TXT")
 class TXT(Callback):
     def init(self):

@@ -161,11 +161,10 @@ class Solver:
         v = self.units.unit_scale(q.unit)
         return self.lattice.quantity(name, scale=1.0 / v).cpu().numpy()
 
-    def write_vtk(self, name: str, what: Optional[Sequence[str]], region=None):
-        from .io import vtk
+    def output_fields(self, what: Optional[Sequence[str]]):
+        """(name, array (nz,ny,nx) or (3,nz,ny,nx), ncomp) of the selected flag groups and
+        quantities (SI units) on this rank's slab (reference vtkWriteLattice selection)"""
         lat = self.lattice
-        fn = self.out_iter_file(name, ".vti")
-        log.output(f"{self.iter:8d} it writing vtk {fn}")
         allq = what is None or "all" in what
         fields = []
         flags = lat.get_flags()
@@ -186,6 +185,14 @@ class Solver:
                     fields.append((q.name, a, 3))
                 else:
                     fields.append((q.name, a[0], 1))
+        return fields
+
+    def write_vtk(self, name: str, what: Optional[Sequence[str]], region=None):
+        from .io import vtk
+        lat = self.lattice
+        fn = self.out_iter_file(name, ".vti")
+        log.output(f"{self.iter:8d} it writing vtk {fn}")
+        fields = self.output_fields(what)
         sx, sy, sz = lat.slab.offset
         nx, ny, nz = lat.shape
         reg = (sx, sy, sz, nx, ny, nz)
@@ -201,6 +208,38 @@ class Solver:
             pieces = [(r, n) for r, n in zip(regs, names) if r is not None]
             meta = [(nme, vtk._VTK_T[np.asarray(a).dtype], nc) for nme, a, nc in fields]
             vtk.write_pvti(fn[:-4] + ".pvti", region, pieces, meta, spacing=spacing)
+        return 0
+
+    def write_xdmf(self, name: str, what: Optional[Sequence[str]], region=None, double: bool = True):
+        """HDF5-callback output without libhdf5: one raw little-endian binary file holding
+        every selected field of the region (each rank pwrite()s its own slab rows) and an
+        XDMF sidecar that ParaView/VisIt open directly (reference hdf5WriteLattice + XDMF,
+        src/hdf5Lattice.cpp:26-339)."""
+        from .io import xdmf
+        lat = self.lattice
+        fields = self.output_fields(what)
+        region = region or self.total
+        sx, sy, sz = lat.slab.offset
+        nx, ny, nz = lat.shape
+        sub = _crop(fields, (sx, sy, sz, nx, ny, nz), region)
+        base = self.out_iter_file(name, "")
+        spacing = 1.0 / self.units.alt("1m") if self.units.alt("1m") != 0 else 1.0
+        dt = np.float64 if double else np.float32
+        meta = [(n, (np.dtype(dt) if np.asarray(a).dtype.kind == "f" else np.asarray(a).dtype), nc)
+                for n, a, nc in fields]
+        layout = xdmf.layout(region, meta)
+        if self.rank == 0:
+            log.output(f"{self.iter:8d} it writing xdmf {base}.xmf")
+            xdmf.create(base + ".bin", layout)
+        self.comm.barrier()
+        if sub is not None:
+            lreg, lfields = sub
+            xdmf.write_piece(base + ".bin", region, lreg, [(n, np.asarray(a).astype(t, copy=False), nc)
+                                                         for (n, a, nc), (_, t, _) in zip(lfields, meta)], layout)
+        self.comm.barrier()
+        if self.rank == 0:
+            xdmf.write_xmf(base + ".xmf", os.path.basename(base) + ".bin", region, layout, spacing,
+                           time=self.iter * self.units.alt("1s") if self.units.alt("1s") else self.iter)
         return 0
 
     def write_txt(self, name: str, what: Optional[Sequence[str]], gzip: bool = False):

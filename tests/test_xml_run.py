@@ -113,3 +113,22 @@ def test_deprecated_params_rewrite():
     ps = root.findall("Model/Param")
     assert [(p.get("name"), p.get("value"), p.get("zone")) for p in ps] == [
         ("nu", "0.1", None), ("psi_bc", "0.025V", "wall"), ("k", "1", None)]
+
+
+def test_hdf5_xdmf_output(tmp_path):
+    """<HDF5> (reference cbHDF5): cropped fields as XDMF + binary; values equal the VTK
+    output of the same step, precision attribute honoured."""
+    from tclb_amd.io.xdmf import read_field
+    xml = KARMAN.replace('<Solve Iterations="100"/>',
+                         '<HDF5 Iterations="50" dx="10" nx="64" what="U,Rho"/>'
+                         '<HDF5 name="F" Iterations="100" precision="float"/><Solve Iterations="100"/>')
+    run_case(tmp_path, xml)
+    out = tmp_path / "output"
+    x = str(out / "case_HDF5_P00_00000100.xmf")
+    u = read_field(x, "U")
+    v = read_vti(str(out / "case_VTK_P00_00000100.vti"))["U"]
+    assert u.shape == (1, 32, 64, 3)
+    assert np.array_equal(u, v[:, :, 10:74, :])
+    assert np.array_equal(read_field(x, "Rho"), read_vti(str(out / "case_VTK_P00_00000100.vti"))["Rho"][:, :, 10:74])
+    f = read_field(str(out / "case_F_P00_00000100.xmf"), "U")
+    assert f.dtype == np.float32 and np.allclose(f, v, rtol=1e-6, atol=1e-9)
