@@ -1,0 +1,201 @@
+"""Discrete adjoint of the lattice time stepping (reference: Lattice::Iteration_Adj,
+IterateTill and the snapshot hierarchy, src/Lattice.cu.Rt:46-61,542-613,843-890).
+
+Every model is differentiable: the AD executor (csrc/include/tclb/executor_ad.hpp)
+re-runs a stage with dual numbers and applies the transposed local Jacobian.  This module
+drives it over actions (reverse stage order, in-place stages pass the adjoint of the
+fields they do not write through), folds ghost-plane contributions back to their owners,
+and runs unsteady adjoints with checkpointed recomputation of the primal trajectory.
+
+Objective:  J = sum over the recorded iterations of the ``Objective`` global (the
+weighted sum of the model's globals, ``<G>InObj`` zonal weights), as in the reference.
+Gradients:  d J / d (initial state) — including parameter densities such as design
+fields, which are carried unchanged through the iterations — and d J / d (selected
+global or zonal settings).
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+from typing import Dict, List, Optional, Sequence
+
+import numpy as np
+import torch
+
+from .ops import abi
+
+
+class AdjointError(RuntimeError):
+    pass
+
+
+class Adjoint:
+    def __init__(self, lat, settings: Sequence[str] = (), zonal: Sequence[str] = ()):
+        if lat.is_gpu:
+            raise AdjointError("the adjoint executor runs on the CPU lattice (device='cpu')")
+        if lat.comm.size > 1:
+            raise AdjointError("adjoint runs are single-rank")
+        if lat.sdtype != torch.float64:
+            raise AdjointError("adjoint needs double precision storage")
+        self.lat = lat
+        self.lib = abi.load_ad(lat.model.name)
+        m = lat.model
+        self.set_mask = np.array([1 if s in settings else 0 for s in lat.gsettings] or [0], dtype=np.int32)
+        self.zon_mask = np.array([1 if s in zonal else 0 for s in lat.zsettings] or [0], dtype=np.int32)
+        self.gset = np.zeros(max(1, len(lat.gsettings)), dtype=np.float64)
+        self.gzon = np.zeros(lat.zvals.size if lat.zvals.size else 1, dtype=np.float64)
+        self.scratch = torch.zeros_like(lat.snaps[0])
+        self.ctx = abi.AdCtx()
+
+    # ------------------------------------------------------------------ one action
+    def _fold_ghosts(self, a: torch.Tensor):
+        """adjoint contributions that landed in ghost planes belong to the periodic image"""
+        lat = self.lat
+        g = lat.g
+        if lat.slab.axis == 2 and lat.gz:
+            n = lat.shape[2]
+            a[:, g + n - g:g + n] += a[:, 0:g]
+            a[:, g:2 * g] += a[:, g + n:2 * g + n]
+            a[:, 0:g] = 0
+            a[:, g + n:2 * g + n] = 0
+        elif lat.slab.axis == 1 and lat.gy:
+            n = lat.shape[1]
+            a[:, :, g + n - g:g + n] += a[:, :, 0:g]
+            a[:, :, g:2 * g] += a[:, :, g + n:2 * g + n]
+            a[:, :, 0:g] = 0
+            a[:, :, g + n:2 * g + n] = 0
+
+    def _ad_stage(self, si: int, inp: torch.Tensor, aout: torch.Tensor, obj_weight: float) -> torch.Tensor:
+        lat = self.lat
+        ain = torch.zeros_like(aout)
+        L = lat._base_launch()
+        lat._sync_settings()
+        L.settings = lat.settings_t.data_ptr()
+        L.zonal = lat.zonal_t.data_ptr()
+        L.nzones = lat.zvals.shape[1]
+        L.flags = lat.flags.data_ptr()
+        L.in_ = inp.data_ptr()
+        L.out = self.scratch.data_ptr()
+        L.stage = si
+        L.glob = 1
+        L.iter = lat.iter
+        L.globals_ = lat.globals_t.data_ptr()
+        c = self.ctx
+        c.aout = aout.data_ptr()
+        c.ain = ain.data_ptr()
+        c.gset = self.gset.ctypes.data
+        c.gzon = self.gzon.ctypes.data
+        c.set_mask = self.set_mask.ctypes.data
+        c.zon_mask = self.zon_mask.ctypes.data
+        c.obj_weight = obj_weight
+        c.overflow = 0
+        L.ext[5] = ctypes.cast(ctypes.pointer(c), ctypes.c_void_p)
+        if lat.turb_t is not None:
+            L.ext[0] = lat.turb_t.data_ptr()
+            L.next[0] = lat.turb_t.shape[0]
+        if lat.cuts is not None:
+            L.ext[1] = lat.cuts.data_ptr()
+            L.next[1] = lat.cuts.numel()
+        self.lib.run(L)
+        if c.overflow:
+            raise AdjointError(f"model {lat.model.name}: a node needed more than {self.lib.tangents} AD tangents")
+        self._fold_ghosts(ain)
+        return ain
+
+    def step_back(self, a_next: torch.Tensor, action: str = "Iteration", obj_weight: float = 1.0) -> torch.Tensor:
+        """adjoint of one `action` applied to the current primal state (snapshot cur):
+        given a_next = dJ/d(state after the action) return dJ/d(state before), adding
+        this step's Objective derivative (weight obj_weight) and setting gradients."""
+        lat = self.lat
+        m = lat.model
+        act = m.action(action)
+        src = lat.snaps[lat.cur]
+        # forward recompute of the intermediate in-place states of multi-stage actions
+        inputs: List[torch.Tensor] = [src]
+        if len(act.stages) > 1:
+            saved = lat.cur
+            tmp = lat.snaps[1 - lat.cur].clone()
+            glob = lat.globals_t.clone()
+            dst = lat.snaps[1 - lat.cur]
+            for k, sname in enumerate(act.stages[:-1]):
+                si = m.stage_index(sname)
+                lat._launch_stage(si, src if k == 0 else dst, dst, False)
+                lat._halo_finish(lat._halo_start(dst, lat._saved_fields(m.stage(sname))))
+                inputs.append(dst.clone())
+            lat.snaps[1 - saved].copy_(tmp)
+            lat.globals_t.copy_(glob)
+        a = a_next
+        for k in range(len(act.stages) - 1, -1, -1):
+            st = m.stage(act.stages[k])
+            si = m.stage_index(act.stages[k])
+            saved = lat._saved_fields(st)
+            aout = torch.zeros_like(a)
+            aout[saved] = a[saved]
+            ain = self._ad_stage(si, inputs[k], aout, obj_weight)
+            if k > 0:
+                keep = a.clone()
+                keep[saved] = 0          # written in place: the old values are overwritten
+                a = ain + keep
+            else:
+                a = ain                  # B's unwritten fields do not depend on A
+        return a
+
+    # ------------------------------------------------------------------ unsteady
+    def unsteady(self, steps: int, action: str = "Iteration", checkpoint: int = 0,
+                 a_final: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """run `steps` primal iterations from the current state recording checkpoints,
+        then sweep backwards; returns dJ/d(initial state).  The primal ends at its final
+        state (as the reference's record/rewind leaves it)."""
+        lat = self.lat
+        checkpoint = checkpoint or max(1, int(math.sqrt(steps)))
+        it0 = lat.iter
+        snaps: Dict[int, torch.Tensor] = {0: lat.snaps[lat.cur].clone()}
+        for t in range(steps):
+            lat.iterate(1, glob_last=True, action=action)
+            if (t + 1) % checkpoint == 0 and t + 1 < steps:
+                snaps[t + 1] = lat.snaps[lat.cur].clone()
+        final = lat.snaps[lat.cur].clone()
+        cur_final = lat.cur
+        a = torch.zeros_like(final) if a_final is None else a_final
+        for t in range(steps - 1, -1, -1):
+            base = max(k for k in snaps if k <= t)
+            lat.snaps[lat.cur].copy_(snaps[base])
+            lat.iter = it0 + base
+            for _ in range(t - base):
+                lat.iterate(1, glob_last=False, action=action)
+            lat.iter = it0 + t
+            a = self.step_back(a, action)
+        lat.snaps[cur_final].copy_(final)
+        lat.cur = cur_final
+        lat.iter = it0 + steps
+        self.a0 = a
+        return a
+
+    def steady(self, iterations: int, action: str = "Iteration", tol: float = 0.0) -> torch.Tensor:
+        """fixed-point adjoint at the current (converged) primal state: a <- A^T a + dJ/df"""
+        a = torch.zeros_like(self.lat.snaps[self.lat.cur])
+        for _ in range(iterations):
+            self.gset[:] = 0
+            self.gzon[:] = 0
+            b = self.step_back(a, action)
+            d = float((b - a).abs().max())
+            a = b
+            if tol and d < tol:
+                break
+        self.a0 = a
+        return a
+
+    # ------------------------------------------------------------------ results
+    def field_gradient(self, name: str) -> np.ndarray:
+        """dJ/d(field) on the interior (nz, ny, nx) — e.g. a design parameter density"""
+        lat = self.lat
+        i = lat.model.field_index(name)
+        nx, ny, nz = lat.shape
+        return self.a0[i, lat.gz:lat.gz + nz, lat.gy:lat.gy + ny, :nx].numpy().copy()
+
+    def setting_gradient(self, name: str, zone: Optional[str] = None) -> float:
+        lat = self.lat
+        if name in lat.gsettings:
+            return float(self.gset[lat.gsettings.index(name)])
+        zi = lat.zone_index(zone or "DefaultZone")
+        return float(self.gzon[lat.zsettings.index(name) * lat.zvals.shape[1] + zi])

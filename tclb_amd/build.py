@@ -72,7 +72,8 @@ def _cmd(kind: str, src: str, out: str, gen_dir: str, variant: str = "") -> List
                 "-munsafe-fp-atomics", "-mllvm", "-simplifycfg-sink-common=false",
                 "-Wno-unused-result", "-Wno-pass-failed", *VARIANTS[variant], *incs,
                 src, "-o", out]
-    return [CXX, "-O3", "-std=c++17", "-fPIC", "-shared", "-fopenmp", "-fno-strict-aliasing",
+    opt = "-O2" if kind == "ad" else "-O3"
+    return [CXX, opt, "-std=c++17", "-fPIC", "-shared", "-fopenmp", "-fno-strict-aliasing",
             "-Wno-unused-variable", *incs, src, "-o", out]
 
 

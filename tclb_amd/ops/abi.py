@@ -56,6 +56,54 @@ class Launch(ctypes.Structure):
 PREC = {"double": 0, "float": 1, "mixed": 2}
 
 
+class AdCtx(ctypes.Structure):
+    """mirror of tclb::AdCtx (csrc/include/tclb/ad.hpp)"""
+    _fields_ = [
+        ("aout", ctypes.c_void_p),
+        ("ain", ctypes.c_void_p),
+        ("gset", ctypes.c_void_p),
+        ("gzon", ctypes.c_void_p),
+        ("set_mask", ctypes.c_void_p),
+        ("zon_mask", ctypes.c_void_p),
+        ("obj_weight", ctypes.c_double),
+        ("overflow", ctypes.c_int),
+        ("reserved", ctypes.c_int),
+    ]
+
+
+class AdLib:
+    """the adjoint (AD) executor library of one model: libtclb_<model>_ad.so"""
+
+    def __init__(self, model: str, path: str):
+        self.model = model
+        self.lib = ctypes.CDLL(path, mode=ctypes.RTLD_LOCAL)
+        self._adj = getattr(self.lib, f"tclb_{model}_adjoint")
+        self._adj.argtypes = [ctypes.POINTER(Launch)]
+        self._adj.restype = ctypes.c_int
+        self.tangents = getattr(self.lib, f"tclb_{model}_ad_tangents")()
+        sz = getattr(self.lib, f"tclb_{model}_sizeof_launch")()
+        if sz != ctypes.sizeof(Launch):
+            raise KernelError(f"ABI mismatch for {path}")
+
+    def run(self, L: Launch):
+        r = self._adj(ctypes.byref(L))
+        if r != 0:
+            raise KernelError(f"{self.model}[ad] stage {L.stage} failed: code {r}")
+
+
+def load_ad(model: str) -> AdLib:
+    from .. import build as B
+    key = (model, "ad", "")
+    with _lock:
+        if key in _libs:
+            return _libs[key]
+        path = B.lib_path(model, "ad")
+        B.build_model(model, kinds=("ad",))
+        lib = AdLib(model, path)
+        _libs[key] = lib
+        return lib
+
+
 class KernelError(RuntimeError):
     pass
 
