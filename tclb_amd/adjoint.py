@@ -150,8 +150,10 @@ class Adjoint:
         checkpoint = checkpoint or max(1, int(math.sqrt(steps)))
         it0 = lat.iter
         snaps: Dict[int, torch.Tensor] = {0: lat.snaps[lat.cur].clone()}
+        self.J = 0.0
         for t in range(steps):
             lat.iterate(1, glob_last=True, action=action)
+            self.J += lat.globals.get("Objective", 0.0)
             if (t + 1) % checkpoint == 0 and t + 1 < steps:
                 snaps[t + 1] = lat.snaps[lat.cur].clone()
         final = lat.snaps[lat.cur].clone()

@@ -1,0 +1,353 @@
+"""Adjoint and optimisation handlers (reference: src/Handlers/acUSAdjoint.cpp,
+acSAdjoint.cpp, acOptimize.cpp.Rt, acFDTest.cpp, acObjective.cpp, acThreshold*.cpp,
+acOptSolve, InternalTopology.cpp, conFieldParameter.cpp, OptimalControl.cpp,
+GenericOptimizer.cpp).
+
+Gradients come from the AD adjoint (tclb_amd.adjoint) — available for every model, not
+only Tapenade-processed ones.  Design parameters follow the reference's PAR_GET / PAR_SET /
+PAR_GRAD / PAR_LOWER / PAR_UPPER protocol; the optimiser is SciPy (L-BFGS-B / SLSQP) in
+place of NLopt, maximising the Objective like the reference's nlopt_set_max_objective.
+"""
+from __future__ import annotations
+
+from typing import List
+
+import numpy as np
+
+from ..utils.log import log
+from .base import (HANDLER_DESIGN, Action, Design, GenericAction, HandlerError, register)
+
+PAR_GET, PAR_SET, PAR_GRAD, PAR_UPPER, PAR_LOWER = range(5)
+
+
+def _designs(solver) -> List[Design]:
+    return [h for h in solver.hands if h.kind & HANDLER_DESIGN]
+
+
+def _get_all(solver, kind):
+    out = []
+    for d in _designs(solver):
+        n = d.number_of_parameters()
+        buf = np.zeros(n)
+        d.parameters(kind, buf)
+        out.append(buf)
+    return np.concatenate(out) if out else np.zeros(0)
+
+
+def _set_all(solver, x):
+    k = 0
+    for d in _designs(solver):
+        n = d.number_of_parameters()
+        d.parameters(PAR_SET, np.asarray(x[k:k + n], dtype=np.float64))
+        k += n
+
+
+# ----------------------------------------------------------------------------- adjoint
+@register("Adjoint")
+class AdjointAction(GenericAction):
+    """<Adjoint type="unsteady|steady"> children </Adjoint>.  Unsteady: the children run
+    the primal (callbacks included); the recorded window is then re-run with checkpoints
+    and swept backwards.  Steady: after the children, a fixed-point adjoint of
+    ``Iterations`` steps at the final primal state.  The objective of the window and the
+    adjoint state are left on the solver for designs/optimisers."""
+
+    def init(self):
+        super().init()
+        from ..adjoint import Adjoint
+        s = self.solver
+        lat = s.lattice
+        typ = self.node.get("type")
+        if typ is None:
+            typ = "steady" if self.node.get("Iterations") is not None else "unsteady"
+        settings = [d.setting for d in _designs(s) if getattr(d, "setting", None) and d.setting in lat.gsettings]
+        zonal = [d.setting for d in _designs(s) if getattr(d, "setting", None) and d.setting in lat.zsettings]
+        state0 = lat.snaps[lat.cur].clone()
+        it0 = lat.iter
+        s_it0 = s.iter
+        self.execute_internal()
+        self.unstack()
+        steps = s.iter - s_it0
+        ad = Adjoint(lat, settings=settings, zonal=zonal)
+        if typ == "unsteady":
+            if steps <= 0:
+                raise HandlerError("No iterations done inside of Unsteady Adjoint! Nothing to do")
+            lat.snaps[lat.cur].copy_(state0)
+            lat.iter = it0
+            ad.unsteady(steps)
+            s.objective = ad.J
+        else:
+            n = int(self.solver.units.alt(self.node.get("Iterations", "100")))
+            ad.steady(n)
+            s.objective = lat.globals.get("Objective", 0.0)
+        s.adjoint = ad
+        log.notice(f"Adjoint ({typ}): objective {s.objective:.10g}")
+        return 0
+
+
+# ----------------------------------------------------------------------------- designs
+def _design_mask(solver):
+    lat = solver.lattice
+    m = lat.model
+    mask = m.group_masks.get("DESIGNSPACE")
+    fl = lat.get_flags()
+    if not mask:
+        return np.ones(fl.shape, dtype=bool)
+    return (fl & mask) != 0
+
+
+@register("InternalTopology")
+class InternalTopology(Design):
+    """parameter densities on DESIGNSPACE nodes, bounds [0, 1] (reference
+    InternalTopology.cpp + Solver::getPar/setPar/getDPar)"""
+
+    def init(self):
+        s = self.solver
+        self.fields = [f for f in s.model.fields if f.parameter and f.is_density]
+        if not self.fields:
+            raise HandlerError(f"model {s.model.name} has no parameter densities")
+        self.mask = _design_mask(s)
+        return 0
+
+    def number_of_parameters(self):
+        return int(self.mask.sum()) * len(self.fields)
+
+    def _view(self, i):
+        lat = self.solver.lattice
+        nx, ny, nz = lat.shape
+        return lat.snaps[lat.cur][i, lat.gz:lat.gz + nz, lat.gy:lat.gy + ny, :nx]
+
+    def parameters(self, kind, data):
+        lat = self.solver.lattice
+        n = int(self.mask.sum())
+        if kind in (PAR_UPPER, PAR_LOWER):
+            data[:] = 1.0 if kind == PAR_UPPER else 0.0
+            return 0
+        for k, f in enumerate(self.fields):
+            i = lat.model.field_index(f.name)
+            if kind == PAR_GET:
+                data[k * n:(k + 1) * n] = self._view(i).numpy()[self.mask]
+            elif kind == PAR_SET:
+                v = self._view(i)
+                a = v.numpy().copy()
+                a[self.mask] = data[k * n:(k + 1) * n]
+                import torch
+                v.copy_(torch.from_numpy(a))
+                lat.exchange()
+            elif kind == PAR_GRAD:
+                ad = getattr(self.solver, "adjoint", None)
+                if ad is None:
+                    raise HandlerError("no adjoint gradient available (run <Adjoint> first)")
+                data[k * n:(k + 1) * n] = ad.field_gradient(f.name)[self.mask]
+        return 0
+
+
+@register("FieldParameter")
+class FieldParameter(InternalTopology):
+    """one named field on DESIGNSPACE nodes, bounds from lower/upper attributes
+    (reference conFieldParameter.cpp)"""
+
+    def init(self):
+        s = self.solver
+        name = self.node.get("field")
+        if name is None:
+            raise HandlerError("FieldParameter needs field=")
+        self.fields = [s.model.field(name)]
+        self.mask = _design_mask(s)
+        self.lower = float(self.node.get("lower", "0"))
+        self.upper = float(self.node.get("upper", "1"))
+        return 0
+
+    def parameters(self, kind, data):
+        if kind == PAR_UPPER:
+            data[:] = self.upper
+            return 0
+        if kind == PAR_LOWER:
+            data[:] = self.lower
+            return 0
+        return super().parameters(kind, data)
+
+
+@register("OptimalControl", "ControlParameter")
+class OptimalControl(Design):
+    """a (zonal) setting as design parameter: what="Setting" or "Setting-Zone"
+    (reference OptimalControl.cpp / conControlParameter.cpp for time-constant controls)"""
+
+    def init(self):
+        what = self.node.get("what") or self.node.get("name")
+        if not what:
+            raise HandlerError("OptimalControl needs what=")
+        self.setting, _, zone = what.partition("-")
+        self.zone = zone or None
+        lat = self.solver.lattice
+        if self.setting not in lat.gsettings and self.setting not in lat.zsettings:
+            raise HandlerError(f"unknown setting {self.setting}")
+        self.lower = float(self.node.get("lower", "-1e30"))
+        self.upper = float(self.node.get("upper", "1e30"))
+        return 0
+
+    def number_of_parameters(self):
+        return 1
+
+    def parameters(self, kind, data):
+        lat = self.solver.lattice
+        if kind == PAR_GET:
+            data[0] = lat.get_setting(self.setting, zone=self.zone)
+        elif kind == PAR_SET:
+            lat.set_setting(self.setting, float(data[0]), zone=self.zone)
+        elif kind == PAR_GRAD:
+            data[0] = self.solver.adjoint.setting_gradient(self.setting, self.zone)
+        elif kind == PAR_UPPER:
+            data[0] = self.upper
+        elif kind == PAR_LOWER:
+            data[0] = self.lower
+        return 0
+
+
+# ----------------------------------------------------------------------------- optimisers
+class _Optimizer(GenericAction):
+    def _evaluate(self, x):
+        s = self.solver
+        lat = s.lattice
+        lat.snaps[lat.cur].copy_(self.state0)
+        lat.iter = self.lat_it0
+        s.iter = self.it0
+        _set_all(s, x)
+        self.execute_internal()
+        self.unstack()
+        J = float(getattr(s, "objective", lat.globals.get("Objective", 0.0)))
+        g = _get_all(s, PAR_GRAD)
+        self.evals += 1
+        self.history.append(J)
+        log.notice(f"{self.node.tag} evaluation {self.evals}: objective {J:.10g}")
+        return J, g
+
+    def _prepare(self):
+        s = self.solver
+        lat = s.lattice
+        self.evals = 0
+        self.history = s.opt_history = []
+        self.state0 = lat.snaps[lat.cur].clone()
+        self.lat_it0 = lat.iter
+        self.it0 = s.iter
+        x0 = _get_all(s, PAR_GET)
+        if x0.size == 0:
+            raise HandlerError(f"{self.node.tag}: no design parameters defined")
+        lo, hi = _get_all(s, PAR_LOWER), _get_all(s, PAR_UPPER)
+        return x0, lo, hi
+
+
+@register("Optimize")
+class Optimize(_Optimizer):
+    """maximise the Objective over the design parameters (reference acOptimize: NLopt,
+    Method MMA/LBFGS/..., MaxEvaluations, tolerances)"""
+
+    def init(self):
+        super().init()
+        from scipy.optimize import minimize
+        x0, lo, hi = self._prepare()
+        method = (self.node.get("Method", "MMA") or "MMA").upper()
+        sp_method = "SLSQP" if method in ("SLSQP", "COBYLA") else "L-BFGS-B"
+        maxev = int(float(self.node.get("MaxEvaluations", "20")))
+        tol = self.node.get("RelTolerance")
+        res = minimize(lambda x: tuple(-v for v in self._evaluate(x)), x0, jac=True, method=sp_method,
+                       bounds=list(zip(lo, hi)),
+                       options={"maxiter": maxev, **({"maxfun": maxev} if sp_method == "L-BFGS-B" else {})},
+                       tol=float(tol) if tol else None)
+        self.solver.lattice.snaps[self.solver.lattice.cur].copy_(self.state0)
+        _set_all(self.solver, res.x)
+        self.solver.optimum = (-res.fun, res.x)
+        log.notice(f"Optimize finished after {self.evals} evaluations: objective {-res.fun:.10g} ({res.message})")
+        return 0
+
+
+@register("FDTest")
+class FDTest(_Optimizer):
+    """finite-difference check of the adjoint gradient (reference acFDTest): prints and
+    stores (parameter, adjoint, finite difference) rows; order 2/4/6 central differences"""
+
+    def init(self):
+        super().init()
+        x0, _, _ = self._prepare()
+        order = max(2, min(6, int(self.node.get("order", "2"))))
+        order += order % 2
+        h = float(self.node.get("h", "1e-6"))
+        sel = self.node.get("parameters")
+        idx = list(range(x0.size))
+        if sel:
+            a, _, b = sel.partition(":")
+            idx = list(range(int(a or 0), int(b) + 1 if b else x0.size)) if ":" in sel else [int(sel)]
+        J0, g0 = self._evaluate(x0)
+        coef = {2: [(1, 0.5)], 4: [(1, 2 / 3), (2, -1 / 12)], 6: [(1, 0.75), (2, -0.15), (3, 1 / 60)]}[order]
+        rows = []
+        for i in idx:
+            d = 0.0
+            for k, c in coef:
+                xp, xm = x0.copy(), x0.copy()
+                xp[i] += k * h
+                xm[i] -= k * h
+                d += c * (self._evaluate(xp)[0] - self._evaluate(xm)[0]) / h
+            rows.append((i, float(g0[i]), d))
+            log.notice(f"FDTest parameter {i}: adjoint {g0[i]:.10g}  finite difference {d:.10g}")
+        self.solver.fdtest = rows
+        self._evaluate(x0)
+        return 0
+
+
+@register("OptSolve")
+class OptSolve(_Optimizer):
+    """simple steepest ascent with step Descent (reference acOptSolve / ITER_OPT):
+    repeat Iterations times: run the children (with an Adjoint), move the parameters
+    by Descent * gradient within their bounds"""
+
+    def init(self):
+        super().init()
+        x, lo, hi = self._prepare()
+        steps = int(float(self.node.get("Iterations", "10")))
+        descent = float(self.node.get("Descent", str(self.solver.lattice.get_setting("Descent")
+                                                      if "Descent" in self.solver.lattice.gsettings else 1e-3)))
+        for _ in range(steps):
+            J, g = self._evaluate(x)
+            x = np.clip(x + descent * g, lo, hi)
+        self.solver.lattice.snaps[self.solver.lattice.cur].copy_(self.state0)
+        _set_all(self.solver, x)
+        return 0
+
+
+@register("Threshold", "ThresholdNow")
+class Threshold(Action):
+    """topology thresholding of the design parameters: p <- (p > level), level from the
+    ``Level`` attribute or the Threshold setting (reference acThreshold/acThresholdNow)"""
+
+    def init(self):
+        super().init()
+        s = self.solver
+        lvl = self.node.get("Level")
+        level = float(lvl) if lvl is not None else s.lattice.get_setting("Threshold")
+        x = _get_all(s, PAR_GET)
+        lo, hi = _get_all(s, PAR_LOWER), _get_all(s, PAR_UPPER)
+        _set_all(s, np.where(x > level, hi, lo))
+        log.notice(f"Threshold at {level}: {int((x > level).sum())} of {x.size} parameters set to upper bound")
+        return 0
+
+
+@register("Objective")
+class Objective(Action):
+    """<Objective G1="w1" G2="w2"/>: set the <G>InObj weights (zone 0) and the Objective
+    global to sum w*G of the current globals (reference acObjective)"""
+
+    def init(self):
+        super().init()
+        s = self.solver
+        lat = s.lattice
+        obj = 0.0
+        for g in s.model.globals_:
+            w = self.node.get(g.name)
+            if w is None or g.name == "Objective":
+                continue
+            w = float(w)
+            obj += w * lat.globals.get(g.name, 0.0)
+            if f"{g.name}InObj" in lat.zsettings:
+                lat.set_setting(f"{g.name}InObj", w)
+        lat.globals["Objective"] = obj
+        s.objective = obj
+        return 0

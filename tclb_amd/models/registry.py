@@ -82,3 +82,4 @@ register("d3q27_PSM_TRT_NEBB", ".particles.d3q27_psm", trt=True, nebb=True)
 register("d3q27_PSM_MS_NEBB", ".particles.d3q27_psm", ms=True, nebb=True)
 register("d3q27_PSM_KL_NEBB", ".particles.d3q27_psm", kl=True, nebb=True)
 register("d3q27_PSM_NEBB_singlekernel", ".particles.d3q27_psm", nebb=True, singlekernel=True)
+register("d2q9_adj", ".optimization.d2q9_adj")

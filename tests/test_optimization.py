@@ -1,0 +1,71 @@
+"""Adjoint / optimisation XML handlers (tclb_amd/handlers/optimization.py; reference
+src/Handlers/acUSAdjoint.cpp, acFDTest.cpp, acOptimize.cpp.Rt, InternalTopology.cpp,
+OptimalControl.cpp) on the topology-optimisation model d2q9_adj: the FDTest handler's
+adjoint gradients must agree with its own central finite differences, and a few
+optimiser evaluations must not decrease the objective."""
+import os
+import xml.etree.ElementTree as ET
+
+import numpy as np
+
+from tclb_amd import handlers  # noqa: F401
+from tclb_amd.solver import Solver
+
+CASE = """<?xml version="1.0"?>
+<CLBConfig version="2.0" output="output/">
+  <Geometry nx="24" ny="10">
+    <MRT><Box/></MRT>
+    <WVelocity><Box nx="1"/></WVelocity>
+    <EPressure><Box dx="-1"/></EPressure>
+    <Inlet><Box dx="2" nx="1"/></Inlet>
+    <Outlet><Box dx="-3" nx="1"/></Outlet>
+    <DesignSpace name="des"><Box dx="8" nx="6" dy="2" ny="6"/></DesignSpace>
+    <Wall mask="ALL"><Channel/></Wall>
+  </Geometry>
+  <Model>
+    <Param name="Velocity" value="0.01"/>
+    <Param name="nu" value="0.1"/>
+    <Param name="PorocityTheta" value="-2"/>
+    <Param name="Porocity" value="0.4" zone="des"/>
+    <Param name="PressureLossInObj" value="-1"/>
+    <Param name="MaterialPenaltyInObj" value="-0.0001"/>
+  </Model>
+  {design}
+  {body}
+</CLBConfig>"""
+
+
+def run(tmp_path, design, body):
+    os.chdir(tmp_path)
+    root = ET.fromstring(CASE.format(design=design, body=body))
+    s = Solver("d2q9_adj", root, conffile=str(tmp_path / "case.xml"), device="cpu")
+    s.run()
+    return s
+
+
+def test_fdtest_topology(tmp_path):
+    s = run(tmp_path, "<InternalTopology/>",
+            '<FDTest parameters="3:5" h="1e-5"><Adjoint type="unsteady"><Solve Iterations="20"/></Adjoint></FDTest>')
+    assert len(s.fdtest) == 3
+    for i, adj, fd in s.fdtest:
+        assert abs(adj - fd) <= 1e-5 * abs(fd) + 1e-12, (i, adj, fd)
+        assert abs(fd) > 0
+
+
+def test_fdtest_control_setting(tmp_path):
+    s = run(tmp_path, '<OptimalControl what="ForceX"/>',
+            '<FDTest order="4" h="1e-6"><Adjoint type="unsteady"><Solve Iterations="15"/></Adjoint></FDTest>')
+    (_, adj, fd), = s.fdtest
+    assert abs(adj - fd) <= 1e-6 * abs(fd) + 1e-12, (adj, fd)
+
+
+def test_optimize_improves_objective(tmp_path):
+    s = run(tmp_path, "<InternalTopology/>",
+            '<Optimize MaxEvaluations="4" Method="MMA"><Adjoint type="unsteady"><Solve Iterations="10"/></Adjoint></Optimize>'
+            '<Threshold Level="0.5"/>')
+    best, x = s.optimum
+    assert np.isfinite(best) and best >= s.opt_history[0] and len(s.opt_history) >= 2
+    assert x.size == 36 and ((x >= 0) & (x <= 1)).all()
+    w = s.lattice.fields_interior()[s.model.field_index("w")].numpy()
+    des = w[0, 2:8, 8:14]
+    assert set(np.unique(des)).issubset({0.0, 1.0})
