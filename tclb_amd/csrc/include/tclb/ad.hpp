@@ -69,6 +69,12 @@ struct Dual {
   friend TCLB_FN Dual cos(const Dual& a) { return a.chain(std::cos(a.v), -std::sin(a.v)); }
   friend TCLB_FN Dual tan(const Dual& a) { const T t = std::tan(a.v); return a.chain(t, T(1) + t * t); }
   friend TCLB_FN Dual tanh(const Dual& a) { const T t = std::tanh(a.v); return a.chain(t, T(1) - t * t); }
+  friend TCLB_FN Dual sinh(const Dual& a) { return a.chain(std::sinh(a.v), std::cosh(a.v)); }
+  friend TCLB_FN Dual cosh(const Dual& a) { return a.chain(std::cosh(a.v), std::sinh(a.v)); }
+  friend TCLB_FN Dual asin(const Dual& a) { return a.chain(std::asin(a.v), T(1) / std::sqrt(T(1) - a.v * a.v)); }
+  friend TCLB_FN Dual acos(const Dual& a) { return a.chain(std::acos(a.v), T(-1) / std::sqrt(T(1) - a.v * a.v)); }
+  friend TCLB_FN Dual log1p(const Dual& a) { return a.chain(std::log1p(a.v), T(1) / (T(1) + a.v)); }
+  friend TCLB_FN Dual expm1(const Dual& a) { return a.chain(std::expm1(a.v), std::exp(a.v)); }
   friend TCLB_FN Dual atan(const Dual& a) { return a.chain(std::atan(a.v), T(1) / (T(1) + a.v * a.v)); }
   friend TCLB_FN Dual fabs(const Dual& a) { return a.chain(std::fabs(a.v), a.v < T(0) ? T(-1) : T(1)); }
   friend TCLB_FN Dual abs(const Dual& a) { return fabs(a); }

@@ -83,3 +83,6 @@ register("d3q27_PSM_MS_NEBB", ".particles.d3q27_psm", ms=True, nebb=True)
 register("d3q27_PSM_KL_NEBB", ".particles.d3q27_psm", kl=True, nebb=True)
 register("d3q27_PSM_NEBB_singlekernel", ".particles.d3q27_psm", nebb=True, singlekernel=True)
 register("d2q9_adj", ".optimization.d2q9_adj")
+register("d2q9_poison_boltzmann", ".electrokinetic.d2q9_poison_boltzmann")
+register("d2q9_cumulant", ".flow.d2q9_cumulant")
+register("d2q9_les", ".flow.d2q9_les")

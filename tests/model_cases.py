@@ -22,6 +22,8 @@ def collision_value(m):
 CASE_SETTINGS = {
     "d2q9_npe_guo": {"epsilon": 50.0, "nu": 0.1, "n_inf_0": 1.0, "n_inf_1": 1.0, "el": 1.0, "el_kbT": 1.0,
                      "psi_bc": 0.01},
+    "d2q9_poison_boltzmann": {"tau_psi": 1.0, "dt": 1.0, "epsilon": 1.0, "n_inf": 0.02, "z": 1.0, "el": 1.0,
+                              "kb": 1.0, "T": 1.0, "psi_bc": 0.01, "psi0": 0.0},
     "d2q9_kuper": {"Density": 1.0, "Temperature": 0.65, "Magic": 0.005, "FAcc": 1.0, "nu": 0.1666},
     "d3q19_kuper": {"Density": 1.0, "Temperature": 0.65, "Magic": 0.005, "FAcc": 1.0, "nu": 0.1666},
     "d3q27_pf_velocity": {"Density_h": 1.0, "Density_l": 0.1, "sigma": 1e-3, "Viscosity_l": 0.05,

@@ -49,3 +49,27 @@ def test_boltzmann_double_layer():
     assert psi[1] > psi[3] > psi[6] > 0                               # screened potential
     assert abs(psi[20]) < 0.15 * zeta
     assert np.isfinite(lat.quantity("U").numpy()).all()
+
+
+def test_poisson_boltzmann_debye_huckel():
+    """d2q9_poison_boltzmann (reference models/electrokinetic/d2q9_poison_boltzmann): for a
+    small wall potential the steady Poisson-Boltzmann solution between two walls is the
+    Debye-Hueckel profile psi = zeta cosh(kappa (y - yc)) / cosh(kappa h),
+    kappa^2 = 2 n_inf z^2 e^2 / (eps kT)."""
+    ny, zeta, kappa = 41, 1e-3, 0.15
+    lat = Lattice("d2q9_poison_boltzmann", (4, ny, 1), device=torch.device("cpu"), precision="double")
+    m = lat.model
+    fl = np.full((lat.NZ, lat.NY, 4), m.node_type("Collision").value, dtype=np.uint32)
+    fl[:, lat.gy + 0, :] = m.node_type("Wall").value
+    fl[:, lat.gy + ny - 1, :] = m.node_type("Wall").value
+    lat.set_flags(fl)
+    for k, v in {"tau_psi": 1.0, "dt": 1.0, "epsilon": 1.0, "n_inf": kappa ** 2 / 2, "z": 1.0, "el": 1.0,
+                 "kb": 1.0, "T": 1.0, "psi_bc": zeta, "psi0": 0.0}.items():
+        lat.set_setting(k, v)
+    lat.init()
+    lat.iterate(1500)
+    psi = lat.quantity("Psi").numpy()[0, 0, :, 1]
+    y = np.arange(ny)
+    exact = zeta * np.cosh(kappa * (y - (ny - 1) / 2)) / np.cosh(kappa * (ny - 1) / 2)
+    assert np.abs(psi - exact)[1:-1].max() < 0.01 * zeta, np.abs(psi - exact)[1:-1].max() / zeta
+    assert lat.quantity("Subiter").numpy().max() > 0

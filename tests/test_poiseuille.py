@@ -11,6 +11,7 @@ CASES = {
     "d3q19": ((4, 18, 4), {"ForceX": 1e-6}, "nu"),
     "d2q9": ((4, 18, 1), {"GravitationX": 1e-6}, "Viscosity"),
     "d2q9_SRT": ((4, 18, 1), {"GravitationX": 1e-6}, "nu"),
+    "d2q9_cumulant": ((4, 18, 1), {"ForceX": 1e-6}, "nu"),
     "d3q27_cumulant": ((4, 18, 4), {"ForceX": 1e-6}, "nu"),
     "d3q19_les": ((4, 18, 4), {"ForceX": 1e-6}, "nu"),
     "auto_d3q19_BGK": ((4, 18, 4), {"ForceX": 1e-6}, "Viscosity"),
@@ -53,3 +54,32 @@ def test_poiseuille(model):
     sel = slice(1, ny - 1)
     err = np.abs(prof[sel] - ana[sel]).max() / ana[sel].max()
     assert err < 0.02, (model, err, prof[sel][:4], ana[sel][:4])
+
+
+@pytest.mark.parametrize("model,extra", [("d2q9_les", {"Smag": 0.0}), ("d2q9_les", {"Smag": 0.16}),
+                                         ("d2q9_cumulant", {"nubuffer": 1.0 / 6.0})])
+def test_inlet_channel_develops_parabola(model, extra):
+    """Zou/He velocity inlet (WVelocity) + pressure outlet (EPressure): downstream the
+    profile is the parabola carrying the inlet flux (2-D models without a body force)."""
+    nx, ny, U0 = 48, 18, 0.01
+    lat = Lattice(model, (nx, ny, 1))
+    m = lat.model
+    fl = np.full((lat.NZ, lat.NY, nx), m.node_type("MRT").value, dtype=np.uint32)
+    fl[:, :, 0] = m.node_type("WVelocity").value | m.node_type("MRT").value
+    fl[:, :, nx - 1] = m.node_type("EPressure").value | m.node_type("MRT").value
+    fl[:, lat.gy + 0, :] = m.node_type("Wall").value
+    fl[:, lat.gy + ny - 1, :] = m.node_type("Wall").value
+    lat.set_flags(fl)
+    lat.set_setting("nu", 1.0 / 6.0)
+    lat.set_setting("Velocity", U0)
+    for k, v in extra.items():
+        lat.set_setting(k, v)
+    lat.init()
+    lat.iterate(4000, glob_last=False)
+    u = lat.quantity("U").numpy()[0][0]          # (ny, nx)
+    prof = u[1:ny - 1, 36]
+    h = ny - 2                                   # walls on the node rows 0 and ny-1
+    y = np.arange(1, ny - 1) - 0.5
+    ana = 6 * U0 * y * (h - y) / h ** 2
+    assert np.isfinite(u).all()
+    assert np.abs(prof - ana).max() < 0.03 * ana.max(), (prof, ana)
