@@ -429,7 +429,13 @@ class Lattice:
         L.iter = self.iter
         L.reserved1 = max(1, self.iter - self.average_start)
         L.stream = self._stream()
-        self.lib.quantity(L, self.prec)
+        if self.particles is not None:   # quantities may look at particles (e.g. Checks)
+            self.particles.pre_stage(self)
+        try:
+            self.lib.quantity(L, self.prec)
+        finally:
+            if self.particles is not None:
+                self.particles.detach(self)
         L.reserved0 = 0
         return out
 

@@ -33,17 +33,45 @@ def d2q9_mrt_basis():
     return B
 
 
-def build(bc: bool = False, autosym: int = 0) -> Model:
-    m = Model("d2q9", dims=2, family="flow", reference="models/flow/d2q9",
-              description="D2Q9 MRT (weighted orthogonal basis) with Zou/He and symmetry boundaries")
+def build(bc: bool = False, autosym: int = 0, par: bool = False, part: bool = False) -> Model:
+    """par: d2q9_par (reference models/flow/d2q9_par) — the node momentum is stored in
+    parameter densities ux, uy by a CalcU stage and overwritten with the rigid-body
+    velocity of covering particles in a particle stage CalcF (velocity imposition, no
+    force feedback).  part: d2q9_part (models/flow/d2q9_part) — single particle stage;
+    the velocity mismatch to covering particles is removed from the fluid and applied to
+    the particles as force."""
+    name = "d2q9_part" if part else ("d2q9_par" if par else "d2q9")
+    m = Model(name, dims=2, family="flow", reference=f"models/flow/{name}",
+              description="D2Q9 MRT (weighted orthogonal basis) with Zou/He and symmetry boundaries"
+              + (", particle velocity coupling" if par or part else ""))
     shifts = [4 / 9] + [1 / 9] * 4 + [1 / 36] * 4
     for i, (x, y) in enumerate(U9):
         m.add_density(f"f[{i}]", int(x), int(y), 0, group="f", shift=shifts[i])
     if bc:
         m.add_density("BC[0]", group="BC", parameter=True)
         m.add_density("BC[1]", group="BC", parameter=True)
+    if par or part:
+        for n in ("ux", "uy", "sol"):
+            m.add_density(n, group="u", parameter=True)
+    if part:
+        for n in ("thx", "thy", "thz"):
+            m.add_density(n, group="th")
     m.add_quantity("Rho", unit="kg/m3")
     m.add_quantity("U", unit="m/s", vector=True)
+    if par or part:
+        m.add_quantity("Solid", unit="1")
+    if part:
+        m.add_quantity("Checks", unit="1")
+        m.add_quantity("Thread", unit="1", vector=True)
+    if par:
+        m.add_stage("BaseIteration", "Run", save_fields=["f"], load_densities=["f", "u"])
+        m.add_stage("CalcU", "CalcU", save_fields=["ux", "uy", "sol"], load_densities=["f"])
+        m.add_stage("CalcF", "CalcF", save_fields=["ux", "uy", "sol"], load_densities=["u"], particle=True)
+        m.add_stage("BaseInit", "Init", save_fields=True, init=True)
+        m.add_action("Iteration", ["BaseIteration", "CalcU", "CalcF"])
+        m.add_action("Init", ["BaseInit", "CalcU", "CalcF"])
+    if part:
+        m.add_stage("BaseIteration", "Run", load_densities=True, save_fields=True, particle=True)
     m.add_setting("RelaxationRate", comment="one over relaxation time", S2="1-RelaxationRate")
     m.add_setting("Viscosity", default=0.16666666, comment="viscosity", RelaxationRate="1.0/(3*Viscosity + 0.5)")
     m.add_setting("VelocityX", default=0, comment="inlet/outlet/init velocity", zonal=True, unit="m/s")
@@ -64,7 +92,7 @@ def build(bc: bool = False, autosym: int = 0) -> Model:
     m.add_node_type("Solid", "BOUNDARY")
     m.add_node_type("Wall", "BOUNDARY")
     m.add_node_type("MRT", "COLLISION")
-    m.options = {"bc": bc, "autosym": autosym}
+    m.options = {"bc": bc, "autosym": autosym, "par": par, "part": part}
     B = d2q9_mrt_basis()
     eq = mrt_eq(U9, mat=B)
     m.add_codegen(lambda _m: mrt_block("mrt", eq))

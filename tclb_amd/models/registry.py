@@ -86,3 +86,7 @@ register("d2q9_adj", ".optimization.d2q9_adj")
 register("d2q9_poison_boltzmann", ".electrokinetic.d2q9_poison_boltzmann")
 register("d2q9_cumulant", ".flow.d2q9_cumulant")
 register("d2q9_les", ".flow.d2q9_les")
+register("d2q9_par", ".flow.d2q9", par=True)
+register("d2q9_par_BC", ".flow.d2q9", par=True, bc=True)
+register("d2q9_part", ".flow.d2q9", part=True)
+register("d2q9_part_BC", ".flow.d2q9", part=True, bc=True)

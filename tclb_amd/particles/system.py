@@ -77,6 +77,10 @@ class ParticleSystem:
         a = acc.cpu().numpy()[:self.n]
         self.force = a[:, 0:3].copy()
         self.torque = a[:, 3:6].copy()
+        self.detach(lat)
+
+    def detach(self, lat):
+        """drop the particle records from the launch (after a stage or a quantity)"""
         lat._L.next[2] = 0
         lat._L.ext[4] = None
         lat._L.next[4] = 0

@@ -101,3 +101,29 @@ def test_solid_grid_gpu_matches_cpu():
     fb, Fb, Tb = _many("cpu", 10 ** 9)
     assert torch.allclose(fa, fb, atol=1e-12)
     assert np.allclose(Fa, Fb, rtol=1e-9, atol=1e-13) and np.allclose(Ta, Tb, rtol=1e-9, atol=1e-13)
+
+
+@pytest.mark.parametrize("name", ["d2q9_par", "d2q9_part"])
+def test_d2q9_particle_velocity_coupling(name):
+    """d2q9_par / d2q9_part (reference models/flow/d2q9_par, d2q9_part): a disk moving
+    through fluid at rest imposes its velocity on the covered nodes and drags the fluid
+    along; d2q9_part also reports the velocity mismatch as a drag force on the disk."""
+    nx, ny, v = 32, 24, 0.01
+    lat = Lattice(name, (nx, ny, 1), device=torch.device("cpu"))
+    lat.set_flags(np.full((lat.NZ, lat.NY, nx), lat.model.node_type("MRT").value, dtype=np.uint32))
+    lat.set_setting("Viscosity", 0.1)
+    sp = SimplePart()
+    sp.add([16.0, 12.0, 0.0], 4.0, v=[v, 0, 0], m=1e9)
+    lat.particles = sp
+    lat.init()
+    lat.iterate(30)
+    u = lat.quantity("U").numpy()[0][0]
+    sol = lat.quantity("Solid").numpy()[0][0]
+    cx = int(round(sp.x[0, 0]))
+    assert sol[12, cx] == 1 and sol[0, 0] == 0
+    if name == "d2q9_par":
+        assert abs(u[12, cx] - v) < 1e-12            # covered node carries the disk velocity
+    else:
+        assert sp.force[0, 0] < 0 and abs(sp.force[0, 1]) < 1e-3 * abs(sp.force[0, 0])
+        assert lat.quantity("Checks").numpy()[0][0][12, cx] >= 1
+    assert u[12, (cx + 8) % nx] > 1e-4                # fluid ahead is pushed along
