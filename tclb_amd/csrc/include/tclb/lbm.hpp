@@ -161,5 +161,42 @@ TCLB_FN void zouhe(R* f, bool pressure, R value, R& rho_out, R* J, const R* vt =
   rho_out = rho;
 }
 
+// Non-equilibrium bounce-back with the tangential momentum taken from the in-plane
+// populations as J_t = -3 sum_{c_AX = 0} c_t f  (the hand-written D3Q27 Zou/He blocks
+// of reference models/flow/experimental/d3q27_BGK/Dynamics.c:174-351,
+// models/nonnewtonian/d3q27_viscoplastic/Dynamics.c:175-325 and
+// models/nonnewtonian/d3q27_kl/Dynamics.c.Rt:144-259 use exactly this closure).
+// rho/J_AX closure as in zouhe(): velocity -> rho = A/(1-K V), pressure -> J_AX = (rho-A)/K.
+template <class L, int AX, int SGN, class R>
+TCLB_FN void nebb_plane(R* f, bool pressure, R value) {
+  R A = R(0);
+  R Jt[3] = {R(0), R(0), R(0)};
+  TCLB_UNROLL for (int i = 0; i < L::Q; i++) {
+    const bool sel = SGN * c_<L>(i, AX) > 0;
+    A += sel ? f[L::opp(i)] : f[i];
+    if (c_<L>(i, AX) == 0) {
+      TCLB_UNROLL for (int t = 0; t < 3; t++)
+        if (t != AX && c_<L>(i, t) != 0) Jt[t] += R(c_<L>(i, t)) * f[i];
+    }
+  }
+  constexpr double K = zh_K<L>(AX, SGN);
+  R J[3];
+  TCLB_UNROLL for (int t = 0; t < 3; t++) J[t] = R(-3) * Jt[t];
+  if (pressure) {
+    J[AX] = (value - A) * R(1.0 / K);
+  } else {
+    const R rho = A / (R(1) - R(K) * value);
+    J[AX] = rho * value;
+  }
+  TCLB_UNROLL for (int i = 0; i < L::Q; i++) {
+    if (SGN * c_<L>(i, AX) > 0) {
+      R cj = R(0);
+      TCLB_UNROLL for (int a = 0; a < 3; a++)
+        if (c_<L>(i, a) != 0) cj += R(c_<L>(i, a)) * J[a];
+      f[i] = f[L::opp(i)] + R(6.0 * L::w(i)) * cj;
+    }
+  }
+}
+
 }  // namespace lbm
 }  // namespace tclb

@@ -21,15 +21,31 @@ def _blocks(_m):
     ])
 
 
-def build(avg: bool = False, ib: bool = False, smag: bool = False) -> Model:
-    m = Model("d3q27_cumulant", dims=3, family="flow", reference="models/flow/d3q27_cumulant",
-              description="D3Q27 cumulant LBM with Galilean correction (+SMAG/AVG/IB options)")
+def build(avg: bool = False, ib: bool = False, smag: bool = False, part: bool = False) -> Model:
+    """``part``: the d3q27_cumulant_part variant (reference models/flow/d3q27_cumulant_part):
+    a particle stage CalcF writes the coupling force density (fx,fy,fz,sol) that the
+    next collision applies instead of the uniform ForceX/Y/Z."""
+    name = "d3q27_cumulant_part" if part else "d3q27_cumulant"
+    m = Model(name, dims=3, family="flow", reference=f"models/flow/{name}",
+              description="D3Q27 cumulant LBM with Galilean correction (+SMAG/AVG/IB options)"
+              + (", particle coupling (CalcF stage)" if part else ""))
     for k in range(27):
         m.add_density(f"f[{k}]", int(U[k, 0]), int(U[k, 1]), int(U[k, 2]), group="f",
                       comment=f"density F{P[k, 0]}{P[k, 1]}{P[k, 2]}")
     m.add_quantity("P", unit="Pa")
     m.add_quantity("U", unit="m/s", vector=True)
     m.add_quantity("Solid", unit="1")
+    if part:
+        for n in ("fx", "fy", "fz", "sol"):
+            m.add_density(n, 0, 0, 0, group="Force", parameter=True)
+        m.add_quantity("F", unit="N/m3", vector=True)
+        m.add_setting("ParticleVelocityLimit", default=0.05, unit="m/s",
+                      comment="(local) particle velocity limit")
+        m.add_stage("BaseIteration", "Run", save_fields=["f", "Force", "avg"], load_densities=["f", "Force", "avg"])
+        m.add_stage("BaseInit", "Init", save_fields=["f", "Force", "avg"])
+        m.add_stage("CalcF", "CalcF", save_fields=["Force"], load_densities=["f", "Force"], particle=True)
+        m.add_action("Iteration", ["BaseIteration", "CalcF"])
+        m.add_action("Init", ["BaseInit", "CalcF"])
     m.add_setting("nu", default=0.16666666, comment="Viscosity")
     m.add_setting("nubuffer", default=0.01, comment="Viscosity in the buffer layer")
     m.add_setting("Velocity", default="0m/s", comment="Inlet velocity", zonal=True, unit="m/s")
@@ -39,15 +55,20 @@ def build(avg: bool = False, ib: bool = False, smag: bool = False) -> Model:
     for a in "XYZ":
         m.add_setting(f"Force{a}", default=0, comment=f"Force {a}")
     m.add_setting("Omega", default=1, comment="relaxation rate for 3rd order cumulants")
-    m.add_global("Density", comment="system density", unit="kg/m3")
+    if part:
+        m.add_setting("Smag", default=0, comment="Smagorinsky coefficient for SGS modeling")
+    else:
+        m.add_global("Density", comment="system density", unit="kg/m3")
     m.add_global("Flux", comment="Volume flux", unit="m3/s")
     m.add_global("Drag", comment="Force exerted on body in X-direction", unit="N")
     m.add_global("Lift", comment="Force exerted on body in Z-direction", unit="N")
     m.add_global("Lateral", comment="Force exerted on body in Y-direction", unit="N")
-    m.add_global("Mass", comment="Integral of density over the domain", unit="kg")
-    for a in "XYZ":
-        m.add_global(f"{a}Momentum", comment=f"Integral of momentum in {a}", unit="kgm/s")
-    for n in ["Buffer", "WVelocityTurbulent", "NVelocity", "SVelocity", "NPressure", "SPressure"]:
+    if not part:
+        m.add_global("Mass", comment="Integral of density over the domain", unit="kg")
+        for a in "XYZ":
+            m.add_global(f"{a}Momentum", comment=f"Integral of momentum in {a}", unit="kgm/s")
+    for n in (["WVelocityTurbulent", "NVelocity", "SVelocity", "NPressure", "SPressure"] if part else
+              ["Buffer", "WVelocityTurbulent", "NVelocity", "SVelocity", "NPressure", "SPressure"]):
         m.add_node_type(n, "BOUNDARY")
     m.add_node_type("NSymmetry", "ADDITIONALS")
     m.add_node_type("SSymmetry", "ADDITIONALS")
@@ -69,10 +90,11 @@ def build(avg: bool = False, ib: bool = False, smag: bool = False) -> Model:
         m.add_field("avgUX", dx=(-1, 1), average=True)
         m.add_field("avgUY", dy=(-1, 1), average=True)
         m.add_field("avgUZ", dz=(-1, 1), average=True)
-    for n in ["EPressure", "EVelocity", "Solid", "Wall", "WPressure", "WVelocity"]:
+    for n in (["EPressure", "EVelocity", "Wall", "WPressure", "WVelocity"] if part else
+              ["EPressure", "EVelocity", "Solid", "Wall", "WPressure", "WVelocity"]):
         m.add_node_type(n, "BOUNDARY")
     m.add_node_type("MRT", "COLLISION")
-    m.options = {"AVG": avg, "IB": ib, "SMAG": smag}
+    m.options = {"AVG": avg, "IB": ib, "SMAG": smag, "PART": part}
     m.add_codegen(_blocks)
     m.set_dynamics("flow/d3q27_cumulant.inc")
     return m

@@ -90,3 +90,12 @@ register("d2q9_par", ".flow.d2q9", par=True)
 register("d2q9_par_BC", ".flow.d2q9", par=True, bc=True)
 register("d2q9_part", ".flow.d2q9", part=True)
 register("d2q9_part_BC", ".flow.d2q9", part=True, bc=True)
+register("d3q27_cumulant_part", ".flow.d3q27_cumulant", part=True)
+register("d3q27_cumulant_part_AVG_IB_SMAG", ".flow.d3q27_cumulant", part=True, avg=True, ib=True, smag=True)
+register("d3q27_BGK", ".flow.d3q27_bgk")
+register("d3q27_BGK_galcor", ".flow.d3q27_bgk", galcor=True)
+register("d3q19_kuper", ".multiphase.d3q19_kuper")
+register("d3q27_kl", ".nonnewtonian.d3q27_kl")
+register("d3q27_kl_OutFlow", ".nonnewtonian.d3q27_kl", outflow=True)
+register("d3q27_viscoplastic", ".nonnewtonian.d3q27_viscoplastic")
+register("d3q27_viscoplastic_OutFlow", ".nonnewtonian.d3q27_viscoplastic", outflow=True)

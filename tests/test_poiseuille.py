@@ -18,6 +18,11 @@ CASES = {
     "auto_d3q19_TRT": ((4, 18, 4), {"ForceX": 1e-6}, "Viscosity"),
     "auto": ((4, 18, 4), {"ForceX": 1e-6}, "Viscosity"),
     "d3q27_cumulant_AVG_IB_SMAG": ((4, 18, 4), {"ForceX": 1e-6}, "nu"),
+    "d3q27_cumulant_part": ((4, 18, 4), {"ForceX": 1e-6}, "nu"),
+    "d3q27_BGK": ((4, 18, 4), {"ForceX": 1e-6}, "nu"),
+    "d3q27_BGK_galcor": ((4, 18, 4), {"ForceX": 1e-6}, "nu"),
+    "d3q27_viscoplastic": ((4, 18, 4), {"ForceX": 1e-6}, "nu"),     # YieldStress = 0: Newtonian
+    "d3q27_kl": ((4, 18, 4), {"GravitationX": 1e-6}, "eta1"),       # sigmaY = eta2 = 0: Newtonian
 }
 
 
