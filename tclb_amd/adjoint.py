@@ -171,6 +171,7 @@ class Adjoint:
         lat.cur = cur_final
         lat.iter = it0 + steps
         self.a0 = a
+        lat.adjoint_state = a
         return a
 
     def steady(self, iterations: int, action: str = "Iteration", tol: float = 0.0) -> torch.Tensor:
@@ -185,6 +186,7 @@ class Adjoint:
             if tol and d < tol:
                 break
         self.a0 = a
+        self.lat.adjoint_state = a
         return a
 
     # ------------------------------------------------------------------ results

@@ -56,8 +56,21 @@ def _deps(model_dir: str, dynamics: Optional[str]) -> List[str]:
     inc = os.path.join(CSRC, "include", "tclb")
     deps = [os.path.join(inc, f) for f in os.listdir(inc) if f.endswith((".hpp", ".h"))]
     deps += [os.path.join(model_dir, f) for f in os.listdir(model_dir) if f.endswith((".hpp", ".hip", ".cpp"))]
-    if dynamics:
-        deps.append(os.path.join(CSRC, "models", dynamics))
+    # the dynamics include and everything it includes from csrc/models (transitively)
+    todo = [dynamics] if dynamics else []
+    seen = set()
+    while todo:
+        rel = todo.pop()
+        p = os.path.join(CSRC, "models", rel)
+        if rel in seen or not os.path.exists(p):
+            continue
+        seen.add(rel)
+        deps.append(p)
+        with open(p) as f:
+            for line in f:
+                s = line.strip()
+                if s.startswith("#include \""):
+                    todo.append(s.split('"')[1])
     return deps
 
 

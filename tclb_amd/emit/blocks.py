@@ -116,6 +116,16 @@ def exprs_function(fname: str, args: Sequence[str], exprs: Sequence[sp.Expr], ou
     return "\n".join([head, body, "  }"])
 
 
+def feq_block(fname: str, U, order: int = 2) -> str:
+    """Equilibrium of a velocity set U in the reference's raw-moment (product-form,
+    J-truncated) construction, MRT_eq(U, rho, J)$feq (src/lib/feq.R:38-82):
+    ``fname(rho, Jx, Jy[, Jz], out)``."""
+    from .symbolic import mrt_eq
+    U = np.asarray(U, dtype=int)
+    eq = mrt_eq(U, orthogonal=False, order=order)
+    return exprs_function(fname, ["rho"] + [str(j) for j in eq.J], eq.feq)
+
+
 def mrt_block(prefix: str, eq: MRTEq, tensor: bool = False) -> str:
     """Moment transform, equilibrium moments and inverse transform of an MRTEq."""
     Q = eq.mat.shape[0]

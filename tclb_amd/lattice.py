@@ -413,6 +413,8 @@ class Lattice:
         q = m.quantities[qi]
         nc = 3 if q.vector else 1
         nx, ny, nz = self.shape
+        if q.adjoint:
+            return self._adjoint_quantity(q, nc) * scale
         out = torch.empty((nc, nz, ny, nx), dtype=self.rdtype, device=self.device)
         self._sync_settings()
         L = self._L
@@ -437,6 +439,33 @@ class Lattice:
             if self.particles is not None:
                 self.particles.detach(self)
         L.reserved0 = 0
+        return out
+
+    def _adjoint_quantity(self, q, nc: int) -> torch.Tensor:
+        """adjoint quantities (reference AddQuantity(adjoint=T)) from the adjoint state of
+        the last Adjoint sweep (zeros before any): <F>B = dJ/dF, RhoB = sum of the
+        adjoint populations of the first density group"""
+        nx, ny, nz = self.shape
+        out = torch.zeros((nc, nz, ny, nx), dtype=self.rdtype, device=self.device)
+        a = getattr(self, "adjoint_state", None)
+        name = q.name
+        if a is None or not (name.endswith("B") or q.adjoint_of):
+            return out
+        a = a[:, self.gz:self.gz + nz, self.gy:self.gy + ny, :nx].to(self.device, self.rdtype)
+        m = self.model
+        if q.adjoint_of:
+            sel = [i for i, f in enumerate(m.fields) if q.adjoint_of in (f.group, f.nicename, f.name)]
+            out[0] = a[sel].sum(0)
+            return out
+        base = name[:-1]
+        idx = [i for i, f in enumerate(m.fields) if base in (f.nicename, f.array) or base.lower() in
+               (f.nicename.lower(), f.array.lower())]
+        if idx:
+            out[0] = a[idx[0]]
+        elif base == "Rho" and m.densities:
+            g = m.densities[0].field.group
+            sel = [m.fields.index(d.field) for d in m.densities if d.field.group == g]
+            out[0] = a[sel].sum(0)
         return out
 
     # ------------------------------------------------------------------ state

@@ -73,6 +73,8 @@ class Quantity:
     unit: str = "1"
     vector: bool = False
     comment: str = ""
+    adjoint: bool = False          # computed from the adjoint state (reference adjoint=T)
+    adjoint_of: Optional[str] = None   # field or density group whose adjoint it reports
 
 
 @dataclass
@@ -229,9 +231,15 @@ class Model:
         self.globals_.append(g)
         return g
 
-    def add_quantity(self, name: str, unit: str = "1", vector: bool = False, comment: str = ""):
-        """AddQuantity (src/conf.R:237-257): requires get<name>() in the dynamics."""
-        q = Quantity(name=name, unit=unit, vector=vector, comment=comment)
+    def add_quantity(self, name: str, unit: str = "1", vector: bool = False, comment: str = "",
+                     adjoint: bool = False, adjoint_of: Optional[str] = None):
+        """AddQuantity (src/conf.R:237-257): requires get<name>() in the dynamics, except
+        for adjoint quantities (``adjoint=True``, reference AddQuantity(adjoint=T)), which
+        the runtime derives from the last adjoint sweep: ``<F>B`` is dJ/d(field F),
+        ``RhoB`` the sum over the adjoint populations of the first density group;
+        ``adjoint_of`` names the field (its adjoint) or density group (sum of adjoints)."""
+        q = Quantity(name=name, unit=unit, vector=vector, comment=comment, adjoint=adjoint,
+                     adjoint_of=adjoint_of)
         self.quantities.append(q)
         return q
 

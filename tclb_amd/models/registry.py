@@ -99,3 +99,7 @@ register("d3q27_kl", ".nonnewtonian.d3q27_kl")
 register("d3q27_kl_OutFlow", ".nonnewtonian.d3q27_kl", outflow=True)
 register("d3q27_viscoplastic", ".nonnewtonian.d3q27_viscoplastic")
 register("d3q27_viscoplastic_OutFlow", ".nonnewtonian.d3q27_viscoplastic", outflow=True)
+register("d2q9_diff", ".experimental.d2q9_diff")
+register("d2q9_lbmpy", ".flow.d2q9_lbmpy")
+register("d2q9_optimalMixing", ".optimization.d2q9_optimalmixing")
+register("d2q9_heat", ".heat.d2q9_heat")

@@ -80,3 +80,48 @@ def test_initial_state_and_zonal_gradient_match_fd():
     assert abs(gf[node] - fd) <= 1e-6 * abs(fd) + 1e-10, (gf[node], fd)
     # J is linear in the objective weight: dJ/dw = J(w=1)
     assert abs(gz - J()) <= 1e-9 * abs(gz)
+
+
+def test_adjoint_quantities_d2q9_diff():
+    """d2q9_diff (reference ADJOINT=1 model with adjoint quantities RhoB, WB): after an
+    unsteady adjoint the WB quantity is dJ/dw and matches a finite difference of the
+    Diff objective with respect to one node's material parameter."""
+    nx, ny, steps = 12, 6, 10
+    lat = Lattice("d2q9_diff", (nx, ny, 1), device=torch.device("cpu"))
+    m = lat.model
+    fl = np.full((lat.NZ, lat.NY, nx), m.node_type("MRT").value, dtype=np.uint32)
+    fl[:, :, 0] |= m.node_type("WPressure").value
+    fl[:, :, nx - 1] |= m.node_type("EPressure").value
+    fl[:, lat.gy:lat.gy + ny, 3] |= m.node_type("Obj2").value
+    fl[:, lat.gy:lat.gy + ny, 8] |= m.node_type("Obj1").value
+    lat.set_flags(fl)
+    for k, v in {"nu0": 0.05, "nu1": 0.2, "InitDensity": 1.0, "InletDensity": 1.1, "OutletDensity": 1.0,
+                 "DiffInObj": 1.0}.items():
+        lat.set_setting(k, v)
+    lat.init()
+    # blend the material: w = 0.5 everywhere
+    wi = m.field_index("w")
+    f = lat.fields_interior().clone()
+    f[wi] = 0.5
+    lat.set_fields_interior(f)
+    assert float(lat.quantity("WB").abs().max()) == 0.0      # no adjoint yet
+    base = lat.snaps[lat.cur].clone()
+    ad = Adjoint(lat)
+    ad.unsteady(steps)
+    wb = lat.quantity("WB")[0, 0].numpy()
+    assert np.abs(wb).max() > 0
+    assert np.allclose(wb, ad.field_gradient("w")[0])
+    rhob = lat.quantity("RhoB")[0, 0].numpy()
+    assert np.isfinite(rhob).all() and np.abs(rhob).max() > 0
+    # finite difference on one node's w
+    y, x, h = ny // 2, 5, 1e-6
+    js = []
+    for s in (+1, -1):
+        lat.snaps[lat.cur].copy_(base)
+        lat.iter = 0
+        g = lat.fields_interior().clone()
+        g[wi, 0, y, x] += s * h
+        lat.set_fields_interior(g)
+        js.append(objective(lat, steps))
+    fd = (js[0] - js[1]) / (2 * h)
+    assert abs(fd - wb[y, x]) < 1e-6 * max(1.0, abs(fd)) + 1e-9, (fd, wb[y, x])

@@ -33,3 +33,42 @@ def test_temperature_mode_decay():
     k = 2 * math.pi / nx
     expect = a * math.exp(-D * k * k * steps)
     assert abs(amp - expect) / expect < 0.02, (amp, expect)
+
+
+def _mode_decay(model, coll, group, settings, D, nx=32, steps=300, quantity="T"):
+    """scale the populations of `group` by 1 + a sin(kx) at rest and compare the decayed
+    amplitude of `quantity` with exp(-D k^2 t)"""
+    lat = Lattice(model, (nx, 4, 1))
+    m = lat.model
+    lat.set_flags(np.full((lat.NZ, lat.NY, nx), m.node_type(coll).value, dtype=np.uint32))
+    for k, v in settings.items():
+        lat.set_setting(k, v)
+    lat.init()
+    f = lat.fields_interior().clone()
+    x = torch.arange(nx, dtype=f.dtype)
+    a = 0.05
+    prof = 1 + a * torch.sin(2 * math.pi * x / nx)
+    sel = [i for i, fl in enumerate(m.fields) if fl.group == group]
+    f[sel] = f[sel] * prof[None, None, None, :]
+    lat.set_fields_interior(f)
+    lat.iterate(steps)
+    Tn = lat.quantity(quantity)[0, 0, 0].numpy()
+    amp = (Tn.max() - Tn.min()) / 2
+    k = 2 * math.pi / nx
+    expect = a * math.exp(-D * k * k * steps)
+    assert abs(amp - expect) / expect < 0.02, (model, amp, expect)
+
+
+def test_d2q9_heat_mode_decay():
+    # D2Q9 MRT temperature, all rates 1/(3 FluidAlfa + 1/2): D = FluidAlfa
+    _mode_decay("d2q9_heat", "MRT", "T", {"FluidAlfa": 0.1, "nu": 0.1, "InitTemperature": 1.0}, 0.1)
+
+
+def test_optimal_mixing_scalar_decay():
+    # D2Q5 BGK scalar (c_s^2 = 1/3): D = K
+    _mode_decay("d2q9_optimalMixing", "MRT", "g", {"K": 0.05, "nu": 0.1, "Temperature": 1.0}, 0.05)
+
+
+def test_d2q9_diff_density_decay():
+    # zero-velocity D2Q9 BGK on w=1 nodes: D = nu1
+    _mode_decay("d2q9_diff", "MRT", "f", {"nu0": 0.3, "nu1": 0.08, "InitDensity": 1.0}, 0.08, quantity="Rho")
