@@ -141,6 +141,33 @@ def mrt_eq(U, rho=None, J=None, sigma2=sp.Rational(1, 3), order=2, orthogonal=Tr
     return ret
 
 
+def mrt_eq_mat(U, mat, rho=None, J=None, sigma2=sp.Rational(1, 3), order=2,
+               correction: Optional[Sequence[sp.Expr]] = None) -> MRTEq:
+    """MRT_eq(U, rho, J, sigma2, order, mat=attr(U,"MAT"), correction=...) of the
+    reference (src/lib/feq.R:38-82): raw product-form equilibrium moments, the optional
+    ``correction`` added to the raw moments of polynomial order > 3 (canonical order),
+    then expressed in the given moment matrix ``mat`` (mat[i, k] = moment k at direction
+    i); ``order`` of every mat moment is the highest raw order it involves."""
+    raw = mrt_eq(U, rho=rho, J=J, sigma2=sigma2, order=order, orthogonal=False)
+    H = list(raw.Req)
+    if correction is not None:
+        hi = [k for k in range(len(H)) if int(raw.order[k]) > 3]
+        if len(hi) != len(correction):
+            raise ValueError("correction of wrong length in mrt_eq_mat")
+        for k, c in zip(hi, correction):
+            H[k] = sp.expand(H[k] + c)
+    M = sp.Matrix(mat)
+    T = raw.mat.inv() * M
+    Q = M.shape[0]
+    ords = []
+    for k in range(Q):
+        nz = [i for i in range(Q) if abs(float(T[i, k])) > 1e-10]
+        ords.append(max(int(raw.order[i]) for i in nz))
+    Req = [sp.expand(e) for e in (sp.Matrix([H]) * T)]
+    feq = [sp.expand(e) for e in (sp.Matrix([Req]) * M.inv())]
+    return MRTEq(Req=Req, mat=M, order=np.array(ords), U=raw.U, p=None, feq=feq, rho=raw.rho, J=raw.J)
+
+
 def weights_from_eq(eq: MRTEq) -> List[sp.Rational]:
     """Lattice weights = feq at rho=1, J=0."""
     subs = {eq.rho: 1}

@@ -103,3 +103,5 @@ register("d2q9_diff", ".experimental.d2q9_diff")
 register("d2q9_lbmpy", ".flow.d2q9_lbmpy")
 register("d2q9_optimalMixing", ".optimization.d2q9_optimalmixing")
 register("d2q9_heat", ".heat.d2q9_heat")
+register("d3q19_adj", ".optimization.d3q19_adj")
+register("d3q19_heat_adj", ".optimization.d3q19_heat_adj")

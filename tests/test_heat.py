@@ -72,3 +72,28 @@ def test_optimal_mixing_scalar_decay():
 def test_d2q9_diff_density_decay():
     # zero-velocity D2Q9 BGK on w=1 nodes: D = nu1
     _mode_decay("d2q9_diff", "MRT", "f", {"nu0": 0.3, "nu1": 0.08, "InitDensity": 1.0}, 0.08, quantity="Rho")
+
+
+def test_d3q19_heat_adj_mode_decay():
+    # D3Q7 with sigma2 = 1/4: D = (tau - 1/2)/4, tau = 3 FluidAlpha + 1/2
+    nx, alpha, steps = 32, 0.1, 200
+    lat = Lattice("d3q19_heat_adj", (nx, 4, 4))
+    m = lat.model
+    lat.set_flags(np.full((lat.NZ, lat.NY, nx), m.node_type("MRT").value, dtype=np.uint32))
+    lat.set_setting("FluidAlpha", alpha)
+    lat.set_setting("nu", 0.1)
+    lat.init()
+    f = lat.fields_interior().clone()
+    x = torch.arange(nx, dtype=f.dtype)
+    a = 0.05
+    prof = 1 + a * torch.sin(2 * math.pi * x / nx)
+    sel = [i for i, fl in enumerate(m.fields) if fl.group == "g"]
+    f[sel] = f[sel] * prof[None, None, None, :]
+    lat.set_fields_interior(f)
+    lat.iterate(steps)
+    Tn = lat.quantity("T")[0, 0, 0].numpy()
+    amp = (Tn.max() - Tn.min()) / 2
+    D = 0.25 * 3 * alpha
+    k = 2 * math.pi / nx
+    expect = a * math.exp(-D * k * k * steps)
+    assert abs(amp - expect) / expect < 0.02, (amp, expect)
