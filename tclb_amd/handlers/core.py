@@ -684,6 +684,9 @@ class Control(GenericAction):
         s = self.solver
         for name, zone, t, v in self.series:
             s.lattice.set_setting(name, float(np.interp(s.iter, t, v)), zone=zone)
+            if s.model.setting(name).zonal:   # slope of the interpolant -> <name>_DT
+                d = float(np.interp(s.iter + 0.5, t, v) - np.interp(s.iter - 0.5, t, v))
+                s.lattice.set_setting_dt(name, d, zone=zone)
         return 0
 
 

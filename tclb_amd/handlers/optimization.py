@@ -332,22 +332,42 @@ class Threshold(Action):
 
 @register("Objective")
 class Objective(Action):
-    """<Objective G1="w1" G2="w2"/>: set the <G>InObj weights (zone 0) and the Objective
-    global to sum w*G of the current globals (reference acObjective)"""
+    """<Objective G1="w1" EfficiencyX="w2"/>: every global is an objective of itself, and a
+    model may define objective functions of the globals (reference AddObjective, the
+    OF_<name> functions of src/Lists.cpp.Rt:18-40).  Objective = sum w_k F_k(globals);
+    the <G>InObj weights (zone 0) are set to sum w_k dF_k/dG (reference acObjective)."""
 
     def init(self):
         super().init()
         s = self.solver
         lat = s.lattice
+        m = s.model
+        gnames = [g.name for g in m.globals_]
+        vals = {g: lat.globals.get(g, 0.0) for g in gnames}
         obj = 0.0
-        for g in s.model.globals_:
-            w = self.node.get(g.name)
-            if w is None or g.name == "Objective":
+        inobj = {g: 0.0 for g in gnames}
+        funcs = [(g, None) for g in gnames if g != "Objective"] + list(getattr(m, "objectives", {}).items())
+        for name, expr in funcs:
+            w = self.node.get(name)
+            if w is None:
                 continue
             w = float(w)
-            obj += w * lat.globals.get(g.name, 0.0)
-            if f"{g.name}InObj" in lat.zsettings:
-                lat.set_setting(f"{g.name}InObj", w)
+            if expr is None:
+                obj += w * vals[name]
+                inobj[name] += w
+            else:
+                import sympy as sp
+                syms = {g: sp.Symbol(g) for g in gnames}
+                e = sp.sympify(expr, locals=syms)
+                sub = {syms[g]: vals[g] for g in gnames}
+                obj += w * float(e.subs(sub))
+                for g in gnames:
+                    d = sp.diff(e, syms[g])
+                    if d != 0:
+                        inobj[g] += w * float(d.subs(sub))
+        for g, v in inobj.items():
+            if f"{g}InObj" in lat.zsettings:
+                lat.set_setting(f"{g}InObj", v)
         lat.globals["Objective"] = obj
         s.objective = obj
         return 0

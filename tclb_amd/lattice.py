@@ -103,6 +103,9 @@ class Lattice:
         self.svals = np.zeros(max(1, len(self.gsettings)), dtype=np.float64)
         self.zone_names: Dict[str, int] = {"DefaultZone": 0}
         self.zvals = np.zeros((max(1, len(self.zsettings)), 1), dtype=np.float64)
+        # time derivatives of the zonal settings (reference ZoneSettings _DT tables), set by
+        # time-dependent controls; uploaded after the values: zonal[(NZS + i) * nzones + z]
+        self.zdt = np.zeros_like(self.zvals)
         self._settings_dirty = True
         self.settings_t = torch.zeros(self.svals.shape, dtype=torch.float64, device=self.device)
         self.zonal_t = torch.zeros(self.zvals.size, dtype=torch.float64, device=self.device)
@@ -146,7 +149,8 @@ class Lattice:
     def _sync_settings(self):
         if self._settings_dirty:
             self.settings_t = torch.as_tensor(self.svals, dtype=torch.float64).to(self.device)
-            self.zonal_t = torch.as_tensor(np.ascontiguousarray(self.zvals).reshape(-1), dtype=torch.float64).to(self.device)
+            z = np.concatenate([self.zvals.reshape(-1), self.zdt.reshape(-1)])
+            self.zonal_t = torch.as_tensor(z, dtype=torch.float64).to(self.device)
             self._settings_dirty = False
         L = self._L
         L.settings = self.settings_t.data_ptr()
@@ -319,6 +323,15 @@ class Lattice:
             for tgt, expr in s.derived.items():
                 self.set_setting(tgt, eval_expr(expr, env), zone=zone)
 
+    def set_setting_dt(self, name: str, value: float, zone: Optional[str] = None):
+        """time derivative of a zonal setting (read by the dynamics as <name>_DT())"""
+        zi = self.zsettings.index(name)
+        if zone is None:
+            self.zdt[zi, :] = float(value)
+        else:
+            self.zdt[zi, self.zone_index(zone)] = float(value)
+        self._settings_dirty = True
+
     def get_setting(self, name: str, zone: Optional[str] = None) -> float:
         s = self.model.setting(name)
         if s is None:
@@ -348,6 +361,7 @@ class Lattice:
         self.zone_names[zone] = zi
         col = self.zvals[:, :1]
         self.zvals = np.concatenate([self.zvals, col], axis=1)
+        self.zdt = np.concatenate([self.zdt, np.zeros_like(col)], axis=1)
         self._settings_dirty = True
         return zi
 

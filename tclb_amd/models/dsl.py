@@ -136,6 +136,7 @@ class Model:
         self.codegen_blocks: List[Callable[["Model"], str]] = []
         self.lattices: Dict[str, str] = {}           # group -> lattice name (weights table)
         self.defines: Dict[str, str] = {}
+        self.objectives: Dict[str, str] = {}        # AddObjective: name -> expression of globals
         self._finalized = False
 
     # ------------------------------------------------------------------ verbs
@@ -242,6 +243,11 @@ class Model:
                      adjoint_of=adjoint_of)
         self.quantities.append(q)
         return q
+
+    def add_objective(self, name: str, expr: str):
+        """AddObjective (src/conf.R:349-360): a named objective function of the globals
+        (sympy-parsable expression), selectable as an attribute of <Objective>."""
+        self.objectives[name] = expr
 
     def add_node_type(self, name: str, group: str):
         """AddNodeType (src/conf.R:259-270)."""
