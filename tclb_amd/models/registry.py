@@ -107,3 +107,4 @@ register("d3q19_adj", ".optimization.d3q19_adj")
 register("d3q19_heat_adj", ".optimization.d3q19_heat_adj")
 register("sw", ".shallowwater.sw")
 register("d2q9_plate", ".moving.d2q9_plate")
+register("d2q9_inc", ".experimental.d2q9_inc")

@@ -24,6 +24,7 @@ CASES = {
     "d3q27_viscoplastic": ((4, 18, 4), {"ForceX": 1e-6}, "nu"),     # YieldStress = 0: Newtonian
     "d3q27_kl": ((4, 18, 4), {"GravitationX": 1e-6}, "eta1"),       # sigmaY = eta2 = 0: Newtonian
     "d2q9_lbmpy": ((4, 18, 1), {"GravitationX": 1e-6}, "nu"),
+    "d2q9_inc": ((4, 18, 1), {"GravitationX": 1e-6}, "nu"),
 }
 
 
