@@ -108,3 +108,5 @@ register("d3q19_heat_adj", ".optimization.d3q19_heat_adj")
 register("sw", ".shallowwater.sw")
 register("d2q9_plate", ".moving.d2q9_plate")
 register("d2q9_inc", ".experimental.d2q9_inc")
+register("d2q9_heat_adj", ".optimization.d2q9_heat_adj")
+register("d2q9_solid", ".multiphase.d2q9_solid")

@@ -30,6 +30,8 @@ CASE_SETTINGS = {
     "d3q27_viscoplastic": {"YieldStress": 1e-4, "nu": 0.1},
     "d2q9_optimalMixing": {"Temperature": 1.0, "MovingWallVelocity": 0.01},
     "sw": {"Height": 1.0, "Gravity": 0.1},
+    "d2q9_solid": {"nu": 0.1, "FluidAlfa": 0.1, "SoluteDiffusion": 0.05, "Temperature": 1.0, "Concentration": 0.5,
+                   "LiquidusSlope": -1.0, "PartitionCoef": 0.5, "C0": 0.5, "Teq": 1.0},
     "d3q27_pf_velocity": {"Density_h": 1.0, "Density_l": 0.1, "sigma": 1e-3, "Viscosity_l": 0.05,
                           "Viscosity_h": 0.05, "M": 0.05, "PhaseField": 1.0, "Radius": 4.0,
                           "CenterX": 12.0, "CenterY": 6.0, "CenterZ": 5.0, "BubbleType": -1.0},

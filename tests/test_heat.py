@@ -97,3 +97,9 @@ def test_d3q19_heat_adj_mode_decay():
     k = 2 * math.pi / nx
     expect = a * math.exp(-D * k * k * steps)
     assert abs(amp - expect) / expect < 0.02, (amp, expect)
+
+
+def test_d2q9_heat_adj_conductivity_blend():
+    # D2Q9 MRT temperature, diffusivity FluidAlpha on w = 1 nodes (Init sets w = 1)
+    _mode_decay("d2q9_heat_adj", "MRT", "T", {"FluidAlpha": 0.08, "SolidAlpha": 0.5, "nu0": 0.1,
+                                               "InitTemperature": 1.0}, 0.08)
