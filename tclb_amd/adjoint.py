@@ -45,6 +45,7 @@ class Adjoint:
         self.gset = np.zeros(max(1, len(lat.gsettings)), dtype=np.float64)
         self.gzon = np.zeros(lat.zvals.size if lat.zvals.size else 1, dtype=np.float64)
         self.scratch = torch.zeros_like(lat.snaps[0])
+        self.series_grads = {}
         self.ctx = abi.AdCtx()
 
     # ------------------------------------------------------------------ one action
@@ -166,13 +167,32 @@ class Adjoint:
             for _ in range(t - base):
                 lat.iterate(1, glob_last=False, action=action)
             lat.iter = it0 + t
+            if lat.zseries:
+                lat.apply_series()
+                before = self.gzon.copy()
             a = self.step_back(a, action)
+            if lat.zseries:
+                self._series_grad(before, lat)
         lat.snaps[cur_final].copy_(final)
         lat.cur = cur_final
         lat.iter = it0 + steps
         self.a0 = a
         lat.adjoint_state = a
         return a
+
+    def _series_grad(self, before: np.ndarray, lat):
+        """attribute this reverse step's zonal-setting gradient to the active entry of
+        each zonal time series (reference zSet gradient tables per time index)"""
+        nz = lat.zvals.shape[1]
+        d = self.gzon - before
+        for key, v in lat.zseries.items():
+            g = self.series_grads.setdefault(key, np.zeros(len(v)))
+            g[lat.series_index(key)] += d[key[0] * nz + key[1]]
+
+    def series_gradient(self, name: str, zone: Optional[str] = None) -> np.ndarray:
+        lat = self.lat
+        key = (lat.zsettings.index(name), lat.zone_index(zone or "DefaultZone"))
+        return self.series_grads.get(key, np.zeros(len(lat.zseries.get(key, [0.0])))).copy()
 
     def steady(self, iterations: int, action: str = "Iteration", tol: float = 0.0) -> torch.Tensor:
         """fixed-point adjoint at the current (converged) primal state: a <- A^T a + dJ/df"""

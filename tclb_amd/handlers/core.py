@@ -4,6 +4,8 @@ from __future__ import annotations
 import collections
 import copy
 import math
+
+import torch
 import os
 import xml.etree.ElementTree as ET
 from typing import List, Optional
@@ -654,15 +656,19 @@ class RunPython(Callback):
 @register("Control")
 class Control(GenericAction):
     """reference conControl (src/Handlers/conControl.cpp:108-257): time-dependent settings.
-    Supported: <CSV file= Time=> column interpolation and <Param name= value=> with
-    ``Iterations`` period; values interpolated linearly every iteration segment."""
+    <CSV file= Time=> columns are sampled at every iteration of a control window of
+    ``Iterations`` steps (linear interpolation in time): zonal settings become zonal time
+    series on the lattice (value and slope <name>_DT active at iter % Iterations, the
+    reference's ZoneSettings tables; optimal-control designs act on them), global
+    settings are set every iteration."""
 
     kind = HANDLER_CALLBACK
 
     def init(self):
         super().init()
         s = self.solver
-        self.series = []  # (setting, zone, times(array), values(array))
+        self.series = []  # global settings: (setting, times(array), values(array))
+        length = int(s.units.alt(self.node.get("Iterations", "0")) or 0)
         for c in self.node:
             if c.tag == "CSV":
                 import csv
@@ -670,23 +676,28 @@ class Control(GenericAction):
                     rows = list(csv.DictReader(f))
                 tcol = c.get("Time", "Time")
                 t = np.array([s.units.alt(r[tcol]) for r in rows])
+                n = length or int(round(t.max())) + 1
                 for col in rows[0]:
                     if col == tcol:
                         continue
-                    if s.model.setting(col) is not None:
-                        self.series.append((col, None, t, np.array([s.units.alt(r[col]) for r in rows])))
+                    name, _, zone = col.partition("-")
+                    st = s.model.setting(name)
+                    if st is None:
+                        continue
+                    v = np.array([s.units.alt(r[col]) for r in rows])
+                    if st.zonal:
+                        s.lattice.set_zone_series(name, np.interp(np.arange(n), t, v), zone=zone or None)
+                    else:
+                        self.series.append((name, t, v))
             elif c.tag == "Param":
                 pass
-        self.every_iter = 1.0
+        self.every_iter = 1.0 if self.series else 0.0
         return 0
 
     def do_it(self):
         s = self.solver
-        for name, zone, t, v in self.series:
-            s.lattice.set_setting(name, float(np.interp(s.iter, t, v)), zone=zone)
-            if s.model.setting(name).zonal:   # slope of the interpolant -> <name>_DT
-                d = float(np.interp(s.iter + 0.5, t, v) - np.interp(s.iter - 0.5, t, v))
-                s.lattice.set_setting_dt(name, d, zone=zone)
+        for name, t, v in self.series:
+            s.lattice.set_setting(name, float(np.interp(s.iter, t, v)))
         return 0
 
 
@@ -778,4 +789,59 @@ class RemoteForceInterface(Action):
         s.lattice.particles = sp
         s.particles = sp
         log.output(f"RemoteForceInterface: {sp.n} particle(s) with built-in SIMPLEPART integrator")
+        return 0
+
+
+@register("Andersen")
+class Andersen(GenericAction):
+    """Anderson acceleration of a fixed-point iteration over the whole lattice state
+    (reference acAndersen.cpp:45-125, "Option B"): each of ``Times`` rounds runs the
+    children once from x to G(x), orthogonalises the newest residual e = G(x) - x against
+    the previous ``Directions`` ones (Gram-Schmidt, the same on the states) and restarts
+    from the least-squares combination of the stored states.  State vectors stay on the
+    device (torch); dot products are all-reduced over ranks."""
+
+    def init(self):
+        super().init()
+        s = self.solver
+        lat = s.lattice
+        if self.node.get("Directions") is None:
+            raise HandlerError("no Directions parameter in Andersen")
+        dirs = int(self.node.get("Directions"))
+        times = int(self.node.get("Times", str(dirs)))
+        eps = float(self.node.get("Eps", "0"))
+
+        def skal(a, b):
+            return lat.comm.allreduce_scalar(float(torch.dot(a.reshape(-1), b.reshape(-1))), "sum")
+
+        X, E, P = [], [], []
+        d = 0
+        self.residuals = []
+        for _ in range(times):
+            x0 = lat.fields_interior().clone()
+            self.execute_internal()
+            self.unstack()
+            e0 = lat.fields_interior().clone() - x0
+            r = skal(e0, e0)
+            self.residuals.append(r)
+            log.notice(f"Residual in Andersen: {r:g}")
+            if not math.isfinite(r) or r < eps:
+                break
+            X.insert(0, x0); E.insert(0, e0); P.insert(0, 1.0)
+            del X[dirs:], E[dirs:], P[dirs:]
+            d = min(d + 1, dirs)
+            for j in range(1, d):
+                a = skal(E[0], E[j])
+                E[0] -= a * E[j]
+                X[0] -= a * X[j]
+                P[0] -= a * P[j]
+            a = math.sqrt(skal(E[0], E[0]))
+            E[0] /= a
+            X[0] /= a
+            P[0] /= a
+            psum = sum(p * p for p in P[:d])
+            nx = sum(X[i] * (P[i] / psum) for i in range(d))
+            lat.set_fields_interior(nx)
+            self.execute_internal()
+            self.unstack()
         return 0

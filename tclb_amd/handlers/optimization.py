@@ -10,6 +10,7 @@ place of NLopt, maximising the Objective like the reference's nlopt_set_max_obje
 """
 from __future__ import annotations
 
+import math
 from typing import List
 
 import numpy as np
@@ -169,8 +170,11 @@ class FieldParameter(InternalTopology):
 
 @register("OptimalControl", "ControlParameter")
 class OptimalControl(Design):
-    """a (zonal) setting as design parameter: what="Setting" or "Setting-Zone"
-    (reference OptimalControl.cpp / conControlParameter.cpp for time-constant controls)"""
+    """a (zonal) setting as design parameter, what="Setting" or "Setting-Zone".  When the
+    zonal setting carries a time series (set by <Control>), every entry of the series is a
+    parameter and its gradient comes per time index from the adjoint (reference
+    OptimalControl.cpp: zSet.get/set/get_grad of length zSet.getLen); otherwise the
+    setting value itself is the single parameter (conControlParameter.cpp)."""
 
     def init(self):
         what = self.node.get("what") or self.node.get("name")
@@ -181,26 +185,218 @@ class OptimalControl(Design):
         lat = self.solver.lattice
         if self.setting not in lat.gsettings and self.setting not in lat.zsettings:
             raise HandlerError(f"unknown setting {self.setting}")
-        self.lower = float(self.node.get("lower", "-1e30"))
-        self.upper = float(self.node.get("upper", "1e30"))
+        self.lower = self.solver.units.alt(self.node.get("lower", "-1e30"))
+        self.upper = self.solver.units.alt(self.node.get("upper", "1e30"))
         return 0
 
+    def _series(self):
+        lat = self.solver.lattice
+        if self.setting in lat.zsettings:
+            return lat.zone_series(self.setting, self.zone)
+        return None
+
     def number_of_parameters(self):
-        return 1
+        v = self._series()
+        return 1 if v is None else len(v)
 
     def parameters(self, kind, data):
         lat = self.solver.lattice
+        v = self._series()
         if kind == PAR_GET:
-            data[0] = lat.get_setting(self.setting, zone=self.zone)
+            data[:] = lat.get_setting(self.setting, zone=self.zone) if v is None else v
         elif kind == PAR_SET:
-            lat.set_setting(self.setting, float(data[0]), zone=self.zone)
+            if v is None:
+                lat.set_setting(self.setting, float(data[0]), zone=self.zone)
+            else:
+                lat.set_zone_series(self.setting, np.asarray(data, dtype=np.float64), zone=self.zone)
         elif kind == PAR_GRAD:
-            data[0] = self.solver.adjoint.setting_gradient(self.setting, self.zone)
+            ad = self.solver.adjoint
+            data[:] = ad.setting_gradient(self.setting, self.zone) if v is None else \
+                ad.series_gradient(self.setting, self.zone)
         elif kind == PAR_UPPER:
-            data[0] = self.upper
+            data[:] = self.upper
         elif kind == PAR_LOWER:
-            data[0] = self.lower
+            data[:] = self.lower
         return 0
+
+
+@register("OptimalControlSecond")
+class OptimalControlSecond(OptimalControl):
+    """time-series control at half resolution: parameter i sets entry 2i, odd entries are
+    linearly interpolated (reference OptimalControlSecond.cpp:70-112)"""
+
+    def number_of_parameters(self):
+        return super().number_of_parameters() // 2
+
+    def _basis(self):
+        n2 = super().number_of_parameters()
+        n = n2 // 2
+        B = np.zeros((n2, n))
+        for i in range(n):
+            if 2 * i < n2:
+                B[2 * i, i] = 1.0
+            if 2 * i + 1 < n2:
+                if i + 1 < n:
+                    B[2 * i + 1, i] = B[2 * i + 1, i + 1] = 0.5
+                else:
+                    B[2 * i + 1, i] = 1.0
+        return B
+
+    def parameters(self, kind, data):
+        n2 = super().number_of_parameters()
+        if kind in (PAR_UPPER, PAR_LOWER):
+            return super().parameters(kind, data)
+        B = self._basis()
+        full = np.zeros(n2)
+        if kind == PAR_GET:
+            super().parameters(PAR_GET, full)
+            data[:] = full[0::2][:len(data)]
+        elif kind == PAR_SET:
+            super().parameters(PAR_SET, B @ np.asarray(data, dtype=np.float64))
+        elif kind == PAR_GRAD:
+            super().parameters(PAR_GRAD, full)
+            data[:] = B.T @ full
+        return 0
+
+
+class _ReducedControl(Design):
+    """a design re-parameterising its single child design through a linear basis B
+    (child = B @ own): SET pushes B p, GRAD pulls B^T g, GET least-squares fits"""
+
+    def init(self):
+        kids = [c for c in self.node if isinstance(c.tag, str)]
+        if len(kids) != 1:
+            raise HandlerError(f"{self.node.tag} needs exactly one child design")
+        from .base import make_handler
+        self.child = make_handler(kids[0], self.solver)
+        if self.child is None or not (self.child.kind & HANDLER_DESIGN):
+            raise HandlerError(f"{self.node.tag} needs a child of design type")
+        self.n2 = self.child.number_of_parameters()
+        self.setting = getattr(self.child, "setting", None)     # for the adjoint's zonal seeds
+        self.zone = getattr(self.child, "zone", None)
+        self.lower = self.solver.units.alt(self.node.get("lower", "-1"))
+        self.upper = self.solver.units.alt(self.node.get("upper", "1"))
+        self.B = self.basis()
+        return 0
+
+    def number_of_parameters(self):
+        return self.B.shape[1]
+
+    def get(self, full):
+        return np.linalg.lstsq(self.B, full, rcond=None)[0]
+
+    def parameters(self, kind, data):
+        if kind == PAR_UPPER:
+            data[:] = self.upper
+        elif kind == PAR_LOWER:
+            data[:] = self.lower
+        elif kind == PAR_SET:
+            self.child.parameters(PAR_SET, self.B @ np.asarray(data, dtype=np.float64))
+        else:
+            full = np.zeros(self.n2)
+            self.child.parameters(kind, full)
+            data[:] = self.get(full) if kind == PAR_GET else self.B.T @ full
+        return 0
+
+
+def bspline_basis(n2: int, n: int, order: int = 3, periodic: bool = False) -> np.ndarray:
+    """B-spline basis of n functions sampled at n2 control instants (reference
+    src/spline.h bspline_b: clamped uniform knots, or periodic wrap)"""
+    def knot(i, nn, k, cut):
+        if not cut:
+            return (i - k) / (nn - k)
+        if i < k + 1:
+            return 0.0
+        if i < nn:
+            return (i - k) / (nn - k)
+        return 1.0
+
+    def bmod(x, p, k, cut):
+        nn = len(p)
+        i = int(math.floor(x * (nn - k))) + k
+        if k > nn - 1:
+            k = nn - 1
+        i = min(max(i, k), nn - 1)
+        for j in range(k, 0, -1):
+            for l in range(j):
+                a = (x - knot(i - l, nn, k, cut)) / (knot(i - l + j, nn, k, cut) - knot(i - l, nn, k, cut))
+                p[i - l] = a * p[i - l] + (1 - a) * p[i - l - 1]
+        return p[i]
+
+    B = np.zeros((n2, n))
+    for j in range(n2):
+        x = j / n2 if periodic else j / max(n2 - 1.0, 1.0)
+        for w in range(n):
+            nn = n + order if periodic else n
+            p = [0.0] * nn
+            p[min(max(w, 0), n - 1)] = 1.0
+            ww = w + nn - order
+            if periodic and ww < nn:
+                p[ww] = 1.0
+            B[j, w] = bmod(x, p, order, not periodic)
+    return B
+
+
+@register("BSpline")
+class BSpline(_ReducedControl):
+    """<BSpline nodes= order= periodic=> child control (reference BSpline.cpp)"""
+
+    def basis(self):
+        n = int(self.node.get("nodes", "10"))
+        return bspline_basis(self.n2, n, int(self.node.get("order", "3")),
+                             self.node.get("periodic", "false").lower() in ("1", "true", "yes"))
+
+
+@register("Fourier")
+class Fourier(_ReducedControl):
+    """<Fourier modes=(odd)> child control: constant + cos/sin pairs over the control
+    window (reference Fourier.cpp)"""
+
+    def basis(self):
+        n = int(self.node.get("modes", "10"))
+        if n % 2 != 1:
+            n += 1
+        j = np.arange(self.n2)
+        B = np.zeros((self.n2, n))
+        for i in range(n):
+            i0, i1 = (i + 1) >> 1, i & 1
+            B[:, i] = np.sin(i0 * math.pi * 2 * j / self.n2) if i1 else np.cos(i0 * math.pi * 2 * j / self.n2)
+        return B
+
+
+@register("RepeatControl")
+class RepeatControl(_ReducedControl):
+    """<RepeatControl length= flip=> child control: a segment of ``length`` entries
+    repeated over the window; with ``flip`` every other repetition is mirrored about the
+    flip level (reference RepeatControl.cpp)"""
+
+    def init(self):
+        self.flip = self.node.get("flip") is not None
+        return super().init()
+
+    def basis(self):
+        n = int(self.solver.units.alt(self.node.get("length", "1")))
+        B = np.zeros((self.n2, n))
+        for j in range(self.n2):
+            odd = self.flip and ((j // n) % 2 == 1)
+            B[j, j % n] = -1.0 if odd else 1.0
+        return B
+
+    def parameters(self, kind, data):
+        if self.flip and kind in (PAR_SET, PAR_GET):
+            lvl = self.solver.units.alt(self.node.get("flip"))
+            n = self.B.shape[1]
+            odd = np.array([((j // n) % 2 == 1) for j in range(self.n2)])
+            if kind == PAR_SET:
+                full = self.B @ np.asarray(data, dtype=np.float64) + np.where(odd, lvl, 0.0)
+                self.child.parameters(PAR_SET, full)
+            else:
+                full = np.zeros(self.n2)
+                self.child.parameters(PAR_GET, full)
+                full = np.where(odd, lvl - full, full)
+                data[:] = np.array([full[i::n].mean() for i in range(n)])
+            return 0
+        return super().parameters(kind, data)
 
 
 # ----------------------------------------------------------------------------- optimisers

@@ -106,6 +106,9 @@ class Lattice:
         # time derivatives of the zonal settings (reference ZoneSettings _DT tables), set by
         # time-dependent controls; uploaded after the values: zonal[(NZS + i) * nzones + z]
         self.zdt = np.zeros_like(self.zvals)
+        # time series of zonal settings (reference ZoneSettings with len > 1):
+        # (setting index, zone index) -> values; entry (iter % len) is active in an iteration
+        self.zseries: Dict[tuple, np.ndarray] = {}
         self._settings_dirty = True
         self.settings_t = torch.zeros(self.svals.shape, dtype=torch.float64, device=self.device)
         self.zonal_t = torch.zeros(self.zvals.size, dtype=torch.float64, device=self.device)
@@ -296,6 +299,8 @@ class Lattice:
         """Reference Lattice::Iterate (src/Lattice.cu.Rt:900-989): globals on the last step."""
         for i in range(n):
             glob = glob_last and i == n - 1
+            if self.zseries:
+                self.apply_series()
             self.run_action(action, glob=glob)
             self.iter += 1
             for cb in self.callbacks:
@@ -330,6 +335,33 @@ class Lattice:
             self.zdt[zi, :] = float(value)
         else:
             self.zdt[zi, self.zone_index(zone)] = float(value)
+        self._settings_dirty = True
+
+    def set_zone_series(self, name: str, values, zone: Optional[str] = None):
+        """time-dependent zonal setting: values[k] is active in iterations with
+        iter % len(values) == k (reference ZoneSettings, ZoneIndex = Iter % len,
+        src/Lattice.cu.Rt:473-477); the time derivative <name>_DT follows the series"""
+        zi = self.zsettings.index(name)
+        z = self.zone_index(zone or "DefaultZone")
+        self.zseries[(zi, z)] = np.asarray(values, dtype=np.float64).copy()
+        self.apply_series()
+
+    def zone_series(self, name: str, zone: Optional[str] = None) -> Optional[np.ndarray]:
+        zi = self.zsettings.index(name)
+        return self.zseries.get((zi, self.zone_index(zone or "DefaultZone")))
+
+    def series_index(self, key) -> int:
+        return self.iter % len(self.zseries[key])
+
+    def apply_series(self):
+        """load the active entries of all zonal time series (and their slopes)"""
+        for key, v in self.zseries.items():
+            n = len(v)
+            k = self.iter % n
+            self.zvals[key] = v[k]
+            if n > 1:
+                lo, hi = max(k - 1, 0), min(k + 1, n - 1)
+                self.zdt[key] = (v[hi] - v[lo]) / max(hi - lo, 1)
         self._settings_dirty = True
 
     def get_setting(self, name: str, zone: Optional[str] = None) -> float:

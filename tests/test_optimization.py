@@ -7,6 +7,7 @@ import os
 import xml.etree.ElementTree as ET
 
 import numpy as np
+import pytest
 
 from tclb_amd import handlers  # noqa: F401
 from tclb_amd.solver import Solver
@@ -69,3 +70,36 @@ def test_optimize_improves_objective(tmp_path):
     w = s.lattice.fields_interior()[s.model.field_index("w")].numpy()
     des = w[0, 2:8, 8:14]
     assert set(np.unique(des)).issubset({0.0, 1.0})
+
+
+def _control_case(tmp_path, design):
+    """inlet velocity as a zonal time series over a 16-iteration control window"""
+    with open(tmp_path / "inlet.csv", "w") as f:
+        f.write("Time,Velocity\n0,0.005\n16,0.015\n")
+    body = ('<Control Iterations="16"><CSV file="inlet.csv" Time="Time"/></Control>'
+            f'{design}'
+            '<FDTest order="4" h="1e-6"><Adjoint type="unsteady"><Solve Iterations="16"/></Adjoint></FDTest>')
+    return run(tmp_path, "", body)
+
+
+def test_time_series_optimal_control_gradient(tmp_path):
+    """OptimalControl of a zonal time series (reference OptimalControl.cpp over
+    zSet.getLen entries): per-time-index adjoint gradients equal finite differences"""
+    s = _control_case(tmp_path, '<OptimalControl what="Velocity" lower="0" upper="0.05"/>')
+    assert len(s.fdtest) == 16
+    for i, adj, fd in s.fdtest:
+        assert abs(adj - fd) <= 1e-6 * max(abs(fd), 1e-8) + 1e-12, (i, adj, fd)
+    assert any(abs(fd) > 0 for _, _, fd in s.fdtest)
+
+
+@pytest.mark.parametrize("design", ['<BSpline nodes="4"><OptimalControl what="Velocity"/></BSpline>',
+                                    '<Fourier modes="3"><OptimalControl what="Velocity"/></Fourier>',
+                                    '<RepeatControl length="4"><OptimalControl what="Velocity"/></RepeatControl>',
+                                    '<OptimalControlSecond what="Velocity"/>'])
+def test_reduced_controls_gradient(tmp_path, design):
+    """BSpline / Fourier / RepeatControl / OptimalControlSecond re-parameterise the series;
+    their chain-ruled adjoint gradients equal finite differences in their own parameters"""
+    s = _control_case(tmp_path, design)
+    assert len(s.fdtest) >= 3
+    for i, adj, fd in s.fdtest:
+        assert abs(adj - fd) <= 1e-6 * max(abs(fd), 1e-8) + 1e-12, (i, adj, fd)
