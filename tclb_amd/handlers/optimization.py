@@ -19,6 +19,7 @@ from ..utils.log import log
 from .base import (HANDLER_DESIGN, Action, Design, GenericAction, HandlerError, register)
 
 PAR_GET, PAR_SET, PAR_GRAD, PAR_UPPER, PAR_LOWER = range(5)
+PAR_X, PAR_Y, PAR_Z, PAR_T = 6, 7, 8, 9          # parameter coordinates (reference vHandler.h:19-22)
 
 
 def _designs(solver) -> List[Design]:
@@ -117,9 +118,23 @@ class InternalTopology(Design):
         nx, ny, nz = lat.shape
         return lat.snaps[lat.cur][i, lat.gz:lat.gz + nz, lat.gy:lat.gy + ny, :nx]
 
+    def coords(self, kind):
+        """x/y/z (global node indices) or t (0) of every parameter"""
+        lat = self.solver.lattice
+        if kind == PAR_T:
+            return np.zeros(self.number_of_parameters())
+        nx, ny, nz = lat.shape
+        ox, oy, oz = lat.slab.offset
+        Z, Y, X = np.meshgrid(np.arange(nz) + oz, np.arange(ny) + oy, np.arange(nx) + ox, indexing="ij")
+        c = {PAR_X: X, PAR_Y: Y, PAR_Z: Z}[kind][self.mask].astype(np.float64)
+        return np.tile(c, len(self.fields))
+
     def parameters(self, kind, data):
         lat = self.solver.lattice
         n = int(self.mask.sum())
+        if kind in (PAR_X, PAR_Y, PAR_Z, PAR_T):
+            data[:] = self.coords(kind)
+            return 0
         if kind in (PAR_UPPER, PAR_LOWER):
             data[:] = 1.0 if kind == PAR_UPPER else 0.0
             return 0
@@ -166,6 +181,93 @@ class FieldParameter(InternalTopology):
             data[:] = self.lower
             return 0
         return super().parameters(kind, data)
+
+
+@register("Extrude")
+class Extrude(Design):
+    """<Extrude direction="x|y|z|t" theta= margin=> child design: the child's parameters
+    are grouped into lines along ``direction`` (equal other coordinates); one parameter
+    per line is the position v of a smooth front, child value = 1/(1 + exp(-(c - v)/theta))
+    (reference conExtrude.cpp: sorted lines, Fun/FunD, GET/UPPER/LOWER front search)."""
+
+    def init(self):
+        kids = [c for c in self.node if isinstance(c.tag, str)]
+        if len(kids) != 1:
+            raise HandlerError("Extrude needs exactly one child design")
+        from .base import make_handler
+        self.child = make_handler(kids[0], self.solver)
+        if self.child is None or not (self.child.kind & HANDLER_DESIGN):
+            raise HandlerError("Extrude needs a child of design type")
+        d = self.node.get("direction")
+        if d not in ("x", "y", "z", "t"):
+            raise HandlerError(f"Extrude needs proper direction - \"{d}\" given")
+        self.dir = "xyzt".index(d)
+        self.theta = self.solver.units.alt(self.node.get("theta", "1"))
+        self.margin = self.solver.units.alt(self.node.get("margin", "1"))
+        self.setting = getattr(self.child, "setting", None)
+        self.zone = getattr(self.child, "zone", None)
+        n2 = self.child.number_of_parameters()
+        C = np.zeros((4, n2))
+        for i, k in enumerate((PAR_X, PAR_Y, PAR_Z, PAR_T)):
+            self.child.parameters(k, C[i])
+        self.C = C
+        others = [i for i in range(4) if i != self.dir]
+        keys = [tuple(C[others, j]) for j in range(n2)]
+        pos = C[self.dir] if self.theta > 0 else -C[self.dir]
+        self.idx = sorted(range(n2), key=lambda j: (keys[j], pos[j]))
+        self.line = np.zeros(n2, dtype=int)          # line number of every child parameter
+        k = 0
+        for a, j in enumerate(self.idx):
+            self.line[j] = k
+            if a + 1 < n2 and keys[self.idx[a + 1]] != keys[j]:
+                k += 1
+        self.n = k + 1 if n2 else 0
+        self.par = np.zeros(self.n)
+        return 0
+
+    def number_of_parameters(self):
+        return self.n
+
+    def _fun(self, x, v):
+        e = np.exp((x - v) / self.theta)
+        return e / (e + 1)
+
+    def _fund(self, x, v):
+        e = np.exp((x - v) / self.theta)
+        return -(e / (e + 1) / (e + 1)) / self.theta
+
+    def parameters(self, kind, data):
+        c = self.C[self.dir]
+        if kind == PAR_SET:
+            self.par = np.asarray(data, dtype=np.float64).copy()
+            self.child.parameters(PAR_SET, self._fun(c, self.par[self.line]))
+        elif kind == PAR_GRAD:
+            g2 = np.zeros(c.size)
+            self.child.parameters(PAR_GRAD, g2)
+            data[:] = np.bincount(self.line, weights=self._fund(c, self.par[self.line]) * g2, minlength=self.n)
+        else:   # GET / UPPER / LOWER: per line, the first position past the front / the extremes
+            vals = np.zeros(c.size)
+            if kind == PAR_GET:
+                self.child.parameters(PAR_GET, vals)
+            out = np.zeros(self.n)
+            st = True
+            k = 0
+            for a, j in enumerate(self.idx):
+                if kind == PAR_UPPER and out[k] < c[j]:
+                    st = True
+                if kind == PAR_LOWER and out[k] > c[j]:
+                    st = True
+                if kind == PAR_GET and vals[j] < 0.5:
+                    st = True
+                if st:
+                    out[k] = c[j]
+                    st = False
+                if a + 1 < len(self.idx) and self.line[self.idx[a + 1]] != k:
+                    k += 1
+                    st = True
+            off = abs(self.margin * self.theta)
+            data[:] = out + off if kind == PAR_UPPER else out - off
+        return 0
 
 
 @register("OptimalControl", "ControlParameter")
@@ -217,6 +319,10 @@ class OptimalControl(Design):
             data[:] = self.upper
         elif kind == PAR_LOWER:
             data[:] = self.lower
+        elif kind == PAR_T:
+            data[:] = np.arange(len(data))
+        elif kind in (PAR_X, PAR_Y, PAR_Z):
+            data[:] = 0.0
         return 0
 
 

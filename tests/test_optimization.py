@@ -103,3 +103,14 @@ def test_reduced_controls_gradient(tmp_path, design):
     assert len(s.fdtest) >= 3
     for i, adj, fd in s.fdtest:
         assert abs(adj - fd) <= 1e-6 * max(abs(fd), 1e-8) + 1e-12, (i, adj, fd)
+
+
+def test_extrude_topology_gradient(tmp_path):
+    """Extrude (reference conExtrude.cpp): one smooth front per design line along x; the
+    chain-ruled adjoint gradient equals finite differences of the front positions"""
+    s = run(tmp_path, '<Extrude direction="x" theta="1.5"><InternalTopology/></Extrude>',
+            '<FDTest h="1e-5" order="4"><Adjoint type="unsteady"><Solve Iterations="20"/></Adjoint></FDTest>')
+    assert len(s.fdtest) == 6              # 6 lines (y = 2..7) through the 6x6 design box
+    for i, adj, fd in s.fdtest:
+        assert abs(adj - fd) <= 1e-5 * abs(fd) + 1e-12, (i, adj, fd)
+        assert abs(fd) > 0
