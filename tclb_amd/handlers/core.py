@@ -845,3 +845,34 @@ class Andersen(GenericAction):
             self.execute_internal()
             self.unstack()
         return 0
+
+
+@register("RunR")
+class RunR(Callback):
+    """reference cbRunR (src/Handlers/cbRunR.cpp:806-872) embeds an R interpreter.  There
+    is no R runtime in this framework: ``python="true"`` runs the element text as
+    RunPython does; anything else stops the case with an explicit error instead of
+    silently skipping the user's code."""
+
+    def init(self):
+        super().init()
+        if self.node.get("python", "false").lower() not in ("true", "1", "yes"):
+            raise HandlerError("RunR: no embedded R interpreter in tclb_amd; "
+                               "use <RunPython> (or RunR python=\"true\") with the equivalent Python code")
+        self.code = (self.node.text or "").strip()
+        return 0
+
+    def do_it(self):
+        return RunPython.do_it(self)
+
+
+@register("ESYSParticle")
+class ESYSParticle(Action):
+    """reference acESYSParticle spawns the ESYS-Particle DEM code over MPMD.  External
+    DEM codes are not part of this build: particle coupling uses the in-process
+    integrator of <RemoteForceInterface integrator="SIMPLEPART">."""
+
+    def init(self):
+        super().init()
+        raise HandlerError("ESYSParticle: external ESYS-Particle coupling is not available; "
+                           "use <RemoteForceInterface integrator=\"SIMPLEPART\">")

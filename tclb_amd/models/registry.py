@@ -110,3 +110,8 @@ register("d2q9_plate", ".moving.d2q9_plate")
 register("d2q9_inc", ".experimental.d2q9_inc")
 register("d2q9_heat_adj", ".optimization.d2q9_heat_adj")
 register("d2q9_solid", ".multiphase.d2q9_solid")
+for _sys in ("AllenCahn", "SIR_SimpleLaplace", "SIR_ModifiedPeng", "SimpleDiffusion", "LinearReaction"):
+    register(f"d2q9_reaction_diffusion_system_{_sys}", ".reaction.d2q9_reaction_diffusion_system", system=_sys)
+    for _opt, _int in (("Trapezoidal", "Trapezoid"), ("Midpoint", "Midpoint"), ("Heun", "Heun"), ("Euler", "Euler")):
+        register(f"d2q9_reaction_diffusion_system_{_sys}_{_opt}", ".reaction.d2q9_reaction_diffusion_system",
+                 system=_sys, integrator=_int)
