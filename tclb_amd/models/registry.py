@@ -115,3 +115,6 @@ for _sys in ("AllenCahn", "SIR_SimpleLaplace", "SIR_ModifiedPeng", "SimpleDiffus
     for _opt, _int in (("Trapezoidal", "Trapezoid"), ("Midpoint", "Midpoint"), ("Heun", "Heun"), ("Euler", "Euler")):
         register(f"d2q9_reaction_diffusion_system_{_sys}_{_opt}", ".reaction.d2q9_reaction_diffusion_system",
                  system=_sys, integrator=_int)
+register("d2q9_lee", ".multiphase.d2q9_lee")
+register("d2q9_pp_LBL", ".multiphase.d2q9_pp_LBL")
+register("d2q9_pp_MCMP", ".multiphase.d2q9_pp_MCMP")
