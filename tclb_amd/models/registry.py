@@ -118,3 +118,5 @@ for _sys in ("AllenCahn", "SIR_SimpleLaplace", "SIR_ModifiedPeng", "SimpleDiffus
 register("d2q9_lee", ".multiphase.d2q9_lee")
 register("d2q9_pp_LBL", ".multiphase.d2q9_pp_LBL")
 register("d2q9_pp_MCMP", ".multiphase.d2q9_pp_MCMP")
+register("d2q9_hb", ".experimental.d2q9_hb")
+register("d2q9_pf_pressureEvolution", ".multiphase.d2q9_pf_pressureEvolution")
