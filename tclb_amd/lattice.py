@@ -508,10 +508,16 @@ class Lattice:
                (f.nicename.lower(), f.array.lower())]
         if idx:
             out[0] = a[idx[0]]
-        elif base == "Rho" and m.densities:
+        elif base in ("Rho", "U") and m.densities:
+            # RhoB / UB: zeroth / first moment of the adjoint populations of the first group
             g = m.densities[0].field.group
-            sel = [m.fields.index(d.field) for d in m.densities if d.field.group == g]
-            out[0] = a[sel].sum(0)
+            dens = [d for d in m.densities if d.field.group == g]
+            sel = [m.fields.index(d.field) for d in dens]
+            if base == "Rho":
+                out[0] = a[sel].sum(0)
+            else:
+                for k, attr in enumerate(("dx", "dy", "dz")[:nc]):
+                    out[k] = sum(a[i] * float(getattr(d, attr)) for i, d in zip(sel, dens) if getattr(d, attr))
         return out
 
     # ------------------------------------------------------------------ state

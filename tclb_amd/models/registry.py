@@ -122,3 +122,4 @@ register("d2q9_hb", ".experimental.d2q9_hb")
 register("d2q9_pf_pressureEvolution", ".multiphase.d2q9_pf_pressureEvolution")
 register("d2q9_AllenCahn_SourceTerm_SOI", ".reaction.d2q9_AllenCahn_SourceTerm_SOI")
 register("d2q9_AllenCahn_SourceTerm_SOI_ExpotentialDecay", ".reaction.d2q9_AllenCahn_SourceTerm_SOI", expdecay=True)
+register("d2q9_kuper_adj", ".optimization.d2q9_kuper_adj")
