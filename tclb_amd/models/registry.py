@@ -123,3 +123,7 @@ register("d2q9_pf_pressureEvolution", ".multiphase.d2q9_pf_pressureEvolution")
 register("d2q9_AllenCahn_SourceTerm_SOI", ".reaction.d2q9_AllenCahn_SourceTerm_SOI")
 register("d2q9_AllenCahn_SourceTerm_SOI_ExpotentialDecay", ".reaction.d2q9_AllenCahn_SourceTerm_SOI", expdecay=True)
 register("d2q9_kuper_adj", ".optimization.d2q9_kuper_adj")
+register("d2q9_pf_velocity", ".multiphase.d2q9_pf_velocity")
+for _o in ("GF", "RT", "Outflow", "GuoCM", "debug", "BGK", "CM"):
+    register(f"d2q9_pf_velocity_{_o}", ".multiphase.d2q9_pf_velocity", **{_o.lower(): True})
+register("d2q9_pf_velocity_autosym", ".multiphase.d2q9_pf_velocity", autosym=1)
