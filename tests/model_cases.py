@@ -32,6 +32,18 @@ CASE_SETTINGS = {
     "sw": {"Height": 1.0, "Gravity": 0.1},
     "d2q9_solid": {"nu": 0.1, "FluidAlfa": 0.1, "SoluteDiffusion": 0.05, "Temperature": 1.0, "Concentration": 0.5,
                    "LiquidusSlope": -1.0, "PartitionCoef": 0.5, "C0": 0.5, "Teq": 1.0},
+    "d2q9_kuper_adj": {"InitDensity": 1.0, "WallDensity": 1.0, "Temperature": 0.65, "Magic": 0.005, "FAcc": 1.0,
+                       "nu": 0.1666, "MagicA": -0.152, "MagicF": 1.0},
+    "d2q9_lee": {"LiquidDensity": 1.0, "VaporDensity": 0.1, "Beta": 0.01, "Kappa": 0.0162, "InitDensity": 0.5,
+                 "WallDensity": 0.5},
+    "d2q9_pp_LBL": {"T": 0.32, "Density": 0.5},
+    "d2q9_pp_MCMP": {"Gc": 1.0, "Density": 1.0, "Density_dry": 0.1},
+    "d2q9_pf_pressureEvolution": {"Density_h": 1.0, "Density_l": 0.1, "sigma": 1e-3, "PhaseField": 1.0,
+                                  "Radius": 5.0, "CenterX": 20.0, "CenterY": 12.0, "BubbleType": -1.0},
+    "d2q9_pf_velocity": {"Density_h": 1.0, "Density_l": 0.1, "sigma": 1e-3, "PhaseField_init": 1.0, "Radius": 5.0,
+                         "CenterX": 20.0, "CenterY": 12.0, "BubbleType": -1.0, "bulk_visc": 0.1666},
+    "d2q9_reaction_diffusion_system_SIR_ModifiedPeng": {"Init_N": 1.0, "Init_S": 0.9, "Init_I": 0.1,
+                                                        "Beta": 0.3, "Beta_w": 0.2, "Gamma": 0.1},
     "d3q27_pf_velocity": {"Density_h": 1.0, "Density_l": 0.1, "sigma": 1e-3, "Viscosity_l": 0.05,
                           "Viscosity_h": 0.05, "M": 0.05, "PhaseField": 1.0, "Radius": 4.0,
                           "CenterX": 12.0, "CenterY": 6.0, "CenterZ": 5.0, "BubbleType": -1.0},
@@ -39,7 +51,9 @@ CASE_SETTINGS = {
 
 
 def case_settings(name):
-    for k, v in CASE_SETTINGS.items():
+    if name in CASE_SETTINGS:
+        return CASE_SETTINGS[name]
+    for k, v in sorted(CASE_SETTINGS.items(), key=lambda kv: -len(kv[0])):
         if name == k or name.startswith(k + "_"):
             return v
     return {}
