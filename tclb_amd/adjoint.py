@@ -94,6 +94,7 @@ class Adjoint:
         if lat.turb_t is not None:
             L.ext[0] = lat.turb_t.data_ptr()
             L.next[0] = lat.turb_t.shape[0]
+            L.time_shift = lat.turb_time_wn
         if lat.cuts is not None:
             L.ext[1] = lat.cuts.data_ptr()
             L.next[1] = lat.cuts.numel()

@@ -65,7 +65,7 @@ struct Launch {
   // accumulator (double[npart][6]), 4,5 = model-specific
   const void* ext[6];
   long long next[6];       // element counts of the ext slots
-  double time_shift;       // spare scalar
+  double time_shift;       // synthetic-turbulence time wave number (Lattice.set_turbulence)
 };
 
 // Periodic wrap helper for non-decomposed axes.

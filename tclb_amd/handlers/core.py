@@ -736,7 +736,12 @@ class SyntheticTurbulenceAction(Action):
             st.set_one_wave(self._wn("Main"), comm=s.comm)
         else:
             raise HandlerError(f"Unknown spectrum {spec}")
-        s.lattice.set_turbulence(st.modes)
+        tw = self._wn("Time")       # reference setTimeScale (acSyntheticTurbulence.cpp:103-109)
+        if tw is None:
+            log.notice("TimeWaveNumber not provided for synthetic turbulence")
+        else:
+            st.time_wn = tw
+        s.lattice.set_turbulence(st.modes, st.time_wn)
         s.turbulence = st
         return 0
 

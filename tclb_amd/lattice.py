@@ -128,6 +128,7 @@ class Lattice:
         self._L = self._base_launch()
         self.callbacks = []
         self.turb_t = None
+        self.turb_time_wn = 0.0
         self.cuts = None
         self.particles = None     # ParticleSystem with pre_stage/post_stage/step hooks
         self.average_start = 0
@@ -164,6 +165,7 @@ class Lattice:
         if self.turb_t is not None:
             L.ext[0] = self.turb_t.data_ptr()
             L.next[0] = self.turb_t.shape[0]
+            L.time_shift = self.turb_time_wn
         if self.cuts is not None:
             L.ext[1] = self.cuts.data_ptr()
             L.next[1] = self.cuts.numel()
@@ -423,9 +425,11 @@ class Lattice:
         full[:, :, :, :nx] = cuts
         self.cuts = torch.from_numpy(full.view(np.int16)).to(self.device)
 
-    def set_turbulence(self, modes: np.ndarray):
-        """synthetic-turbulence modes (n, 7) -> device (Launch.ext[0])"""
+    def set_turbulence(self, modes: np.ndarray, time_wn: float = 0.0):
+        """synthetic-turbulence modes (n, 7) -> device (Launch.ext[0]); the time wave number
+        of time-correlated inflow turbulence travels in Launch.time_shift"""
         self.turb_t = torch.as_tensor(np.ascontiguousarray(modes, dtype=np.float64)).to(self.device)
+        self.turb_time_wn = float(time_wn)
 
     def reset_average(self):
         """reset averaged fields (reference cbAveraging -> resetAverage, src/Lattice.cu.Rt:1360-1365)"""

@@ -127,3 +127,4 @@ register("d2q9_pf_velocity", ".multiphase.d2q9_pf_velocity")
 for _o in ("GF", "RT", "Outflow", "GuoCM", "debug", "BGK", "CM"):
     register(f"d2q9_pf_velocity_{_o}", ".multiphase.d2q9_pf_velocity", **{_o.lower(): True})
 register("d2q9_pf_velocity_autosym", ".multiphase.d2q9_pf_velocity", autosym=1)
+register("d3q27_cumulant_heat", ".heat.d3q27_cumulant_heat")
