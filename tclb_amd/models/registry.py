@@ -128,3 +128,6 @@ for _o in ("GF", "RT", "Outflow", "GuoCM", "debug", "BGK", "CM"):
     register(f"d2q9_pf_velocity_{_o}", ".multiphase.d2q9_pf_velocity", **{_o.lower(): True})
 register("d2q9_pf_velocity_autosym", ".multiphase.d2q9_pf_velocity", autosym=1)
 register("d3q27_cumulant_heat", ".heat.d3q27_cumulant_heat")
+register("d2q9q9_cm_cht", ".heat.d2q9q9_cm_cht")
+for _o in ("OutFlowConvective", "OutFlowNeumann", "AVG", "IBB", "SMAG", "CHT"):
+    register(f"d2q9q9_cm_cht_{_o}", ".heat.d2q9q9_cm_cht", **{_o.lower(): True})

@@ -88,7 +88,7 @@ def test_time_series_optimal_control_gradient(tmp_path):
     s = _control_case(tmp_path, '<OptimalControl what="Velocity" lower="0" upper="0.05"/>')
     assert len(s.fdtest) == 16
     for i, adj, fd in s.fdtest:
-        assert abs(adj - fd) <= 1e-6 * max(abs(fd), 1e-8) + 1e-12, (i, adj, fd)
+        assert abs(adj - fd) <= 1e-6 * max(abs(fd), 1e-8) + 1e-11, (i, adj, fd)   # FD round-off ~1e-12
     assert any(abs(fd) > 0 for _, _, fd in s.fdtest)
 
 
@@ -102,7 +102,7 @@ def test_reduced_controls_gradient(tmp_path, design):
     s = _control_case(tmp_path, design)
     assert len(s.fdtest) >= 3
     for i, adj, fd in s.fdtest:
-        assert abs(adj - fd) <= 1e-6 * max(abs(fd), 1e-8) + 1e-12, (i, adj, fd)
+        assert abs(adj - fd) <= 1e-6 * max(abs(fd), 1e-8) + 1e-11, (i, adj, fd)   # FD round-off ~1e-12
 
 
 def test_extrude_topology_gradient(tmp_path):
