@@ -37,7 +37,9 @@ def test_model_hip_matches_cpu(name):
     for q in a.model.quantities:
         qa, qb = a.quantity(q.name).cpu(), b.quantity(q.name)
         s = qb.abs().max().item() + 1e-300
-        assert torch.allclose(qa, qb, atol=1e-10 * s, rtol=1e-10), q.name
+        # quantities that are differences of O(1) populations (e.g. forces that vanish in
+        # the bulk) carry FMA-contraction noise relative to the populations however small their maximum is
+        assert torch.allclose(qa, qb, atol=1e-10 * s + 1e-12 * scale, rtol=1e-10), (q.name, (qa - qb).abs().max().item())
 
 
 @pytest.mark.gpu
