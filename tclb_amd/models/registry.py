@@ -106,6 +106,7 @@ register("d2q9_heat", ".heat.d2q9_heat")
 register("d3q19_adj", ".optimization.d3q19_adj")
 register("d3q19_heat_adj", ".optimization.d3q19_heat_adj")
 register("d3q19_heat_adj_art", ".optimization.d3q19_heat_adj_art")
+register("d3q19_heat_adj_prop", ".optimization.d3q19_heat_adj_prop")
 register("sw", ".shallowwater.sw")
 register("d2q9_plate", ".moving.d2q9_plate")
 register("d2q9_inc", ".experimental.d2q9_inc")
