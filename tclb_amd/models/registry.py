@@ -50,6 +50,7 @@ register("advection_diffusion2D", ".pde.pde2d", "build_advection_diffusion")
 register("advection_diffusion2D_fields", ".pde.pde2d", "build_advection_diffusion", fields=True)
 register("wave2D", ".pde.pde2d", "build_wave")
 register("d3q27_cumulant", ".flow.d3q27_cumulant")
+register("d3q27_cumulant_qibb_small", ".flow.d3q27_cumulant_qibb_small")
 register("d3q27_cumulant_AVG_IB_SMAG", ".flow.d3q27_cumulant", avg=True, ib=True, smag=True)
 register("d3q19_heat", ".heat.d3q19_heat")
 register("auto", ".flow.auto")
