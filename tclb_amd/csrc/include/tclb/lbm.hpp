@@ -168,7 +168,7 @@ TCLB_FN void zouhe(R* f, bool pressure, R value, R& rho_out, R* J, const R* vt =
 // models/nonnewtonian/d3q27_kl/Dynamics.c.Rt:144-259 use exactly this closure).
 // rho/J_AX closure as in zouhe(): velocity -> rho = A/(1-K V), pressure -> J_AX = (rho-A)/K.
 template <class L, int AX, int SGN, class R>
-TCLB_FN void nebb_plane(R* f, bool pressure, R value) {
+TCLB_FN void nebb_plane(R* f, bool pressure, R value, R* Jout = nullptr, R* rho_out = nullptr) {
   R A = R(0);
   R Jt[3] = {R(0), R(0), R(0)};
   TCLB_UNROLL for (int i = 0; i < L::Q; i++) {
@@ -182,12 +182,15 @@ TCLB_FN void nebb_plane(R* f, bool pressure, R value) {
   constexpr double K = zh_K<L>(AX, SGN);
   R J[3];
   TCLB_UNROLL for (int t = 0; t < 3; t++) J[t] = R(-3) * Jt[t];
+  R rho = value;
   if (pressure) {
     J[AX] = (value - A) * R(1.0 / K);
   } else {
-    const R rho = A / (R(1) - R(K) * value);
+    rho = A / (R(1) - R(K) * value);
     J[AX] = rho * value;
   }
+  if (Jout != nullptr) { Jout[0] = J[0]; Jout[1] = J[1]; Jout[2] = J[2]; }
+  if (rho_out != nullptr) *rho_out = rho;
   TCLB_UNROLL for (int i = 0; i < L::Q; i++) {
     if (SGN * c_<L>(i, AX) > 0) {
       R cj = R(0);

@@ -134,3 +134,6 @@ register("d3q27_cumulant_heat", ".heat.d3q27_cumulant_heat")
 register("d2q9q9_cm_cht", ".heat.d2q9q9_cm_cht")
 for _o in ("OutFlowConvective", "OutFlowNeumann", "AVG", "IBB", "SMAG", "CHT"):
     register(f"d2q9q9_cm_cht_{_o}", ".heat.d2q9q9_cm_cht", **{_o.lower(): True})
+register("d3q27q7_cm_cht", ".heat.d3q27q7_cm_cht")
+for _o in ("OutFlowConvective", "OutFlowNeumann", "AVG", "IBB", "SMAG", "CHT"):
+    register(f"d3q27q7_cm_cht_{_o}", ".heat.d3q27q7_cm_cht", **{_o.lower(): True})

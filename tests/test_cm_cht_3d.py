@@ -1,0 +1,126 @@
+"""d3q27q7_cm_cht: the D3Q7 enthalpy population diffuses with D = conductivity (cp = rho =
+1) under the CM, CM_PROB and BGK heat collisions, buoyancy accelerates the fluid by
+g (rho - B (T - 10)) / rho per step, the equilibrium / anti-bounce-back heaters pin T, and
+every option variant keeps a uniform state at rest (reference
+models/heat/d3q27q7_cm_cht/Dynamics.c.Rt:247-1487)."""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from tclb_amd.lattice import Lattice
+
+
+def _lat(shape, collision="CM", extra=None, model="d3q27q7_cm_cht", **settings):
+    lat = Lattice(model, shape)
+    m = lat.model
+    flags = np.full((lat.NZ, lat.NY, shape[0]), m.node_type(collision).value, dtype=np.uint32)
+    if extra is not None:
+        extra(flags, m)
+    lat.set_flags(flags)
+    for k, v in settings.items():
+        lat.set_setting(k, v)
+    lat.init()
+    return lat
+
+
+@pytest.mark.parametrize("collision", ["CM", "CM_PROB", "BGK"])
+def test_heat_diffusion(collision):
+    nx, k, steps, a = 32, 0.05, 300, 0.05
+    lat = _lat((nx, 2, 2), collision, conductivity=k, InitTemperature=1.0, nu=0.1)
+    m = lat.model
+    f = lat.fields_interior().clone()
+    x = torch.arange(nx, dtype=f.dtype)
+    prof = 1 + a * torch.sin(2 * math.pi * x / nx)
+    sel = [i for i, fl in enumerate(m.fields) if fl.group == "h"]
+    f[sel] = f[sel] * prof[None, None, None, :]
+    lat.set_fields_interior(f)
+    lat.iterate(steps)
+    t = lat.quantity("T")[0, 0, 0].double().numpy()
+    amp = (t.max() - t.min()) / 2
+    kk = 2 * math.pi / nx
+    expect = a * math.exp(-k * kk * kk * steps)
+    assert abs(amp - expect) / expect < 0.03, (collision, amp, expect)
+    assert abs(t.mean() - 1.0) < 1e-10
+
+
+def test_boussinesq_acceleration():
+    n, g, B, T = 20, 1e-5, 0.05, 12.0
+    lat = _lat((4, 4, 4), InitTemperature=T, GravitationZ=g, BoussinesqCoeff=B, nu=0.1, conductivity=0.1)
+    lat.iterate(n)
+    uz = lat.quantity("U")[2].double()
+    a = g * (1 - B * (T - 10.0))
+    expect = n * a + a / 2   # reported U includes F / (2 rho)
+    assert float((uz - expect).abs().max()) < 1e-10, (float(uz.mean()), expect)
+    assert float(lat.quantity("U")[:2].double().abs().max()) < 1e-12
+
+
+def _heater_lat(kind, nx=24):
+    """west slab (x = 0, 1) is a heater zone at T = 1; the bulk starts at T = 0"""
+    lat = Lattice("d3q27q7_cm_cht", (nx, 2, 2))
+    m = lat.model
+    zi = lat.zone_index("heater")
+    flags = np.full((lat.NZ, lat.NY, nx), m.node_type("CM").value, dtype=np.uint32)
+    flags[:, :, :2] |= m.node_type(kind).value | (zi << m.zone_shift)
+    if kind == "HeaterDirichletTemperatureABB":
+        flags[:, :, :2] |= m.node_type("Wall").value
+    lat.set_flags(flags)
+    for k, v in dict(conductivity=0.1, nu=0.1, InitTemperature=0.0).items():
+        lat.set_setting(k, v)
+    lat.set_setting("InitTemperature", 1.0, zone="heater")
+    lat.init()
+    return lat
+
+
+@pytest.mark.parametrize("kind", ["HeaterDirichletTemperatureEQ", "HeaterDirichletTemperatureABB"])
+def test_dirichlet_heater(kind):
+    lat = _heater_lat(kind)
+    lat.iterate(400)
+    t = lat.quantity("T")[0, 0, 0].double().numpy()
+    inner = t[2:12]
+    assert np.all(np.diff(inner) < 0), inner
+    assert 0.0 < inner[-1] < inner[0] < 1.0, inner
+    assert lat.globals["HeatSource"] > 0.0
+
+
+def test_pressure_driven_channel():
+    """W/E pressure planes drive a flow between bounce-back walls; the inflow imposes
+    the inlet temperature on the heat populations"""
+    nx, ny = 24, 9
+
+    def extra(fl, m):
+        fl[:, :, 0] = m.node_type("WPressure").value | m.node_type("CM").value
+        fl[:, :, -1] = m.node_type("EPressure").value | m.node_type("CM").value
+        fl[:, 0, :] = m.node_type("Wall").value
+        fl[:, -1, :] = m.node_type("Wall").value
+
+    lat = Lattice("d3q27q7_cm_cht", (nx, ny, 2))
+    m = lat.model
+    fl = np.full((lat.NZ, lat.NY, nx), m.node_type("CM").value, dtype=np.uint32)
+    extra(fl, m)
+    zi = lat.zone_index("inlet")
+    fl[:, 1:-1, 0] |= zi << m.zone_shift
+    lat.set_flags(fl)
+    lat.set_setting("nu", 0.1)
+    lat.set_setting("conductivity", 0.1)
+    lat.set_setting("Pressure", 1e-4, zone="inlet")
+    lat.set_setting("InitTemperature", 1.0, zone="inlet")
+    lat.init()
+    lat.iterate(600)
+    u = lat.quantity("U")[0, 0].double().numpy()
+    t = lat.quantity("T")[0, 0].double().numpy()
+    mid = u[1:-1, nx // 2]
+    assert mid.min() > 0, mid
+    assert mid[len(mid) // 2] > mid[0], mid          # parabolic-like profile
+    assert 0.0 < t[ny // 2, nx // 2] < 1.0 + 1e-9
+
+
+@pytest.mark.parametrize("variant", ["d3q27q7_cm_cht_OutFlowNeumann", "d3q27q7_cm_cht_OutFlowConvective",
+                                     "d3q27q7_cm_cht_AVG", "d3q27q7_cm_cht_CHT", "d3q27q7_cm_cht_SMAG",
+                                     "d3q27q7_cm_cht_IBB"])
+def test_variants_conserve_uniform_state(variant):
+    lat = _lat((6, 4, 4), model=variant, InitTemperature=1.0, nu=0.1, conductivity=0.1)
+    lat.iterate(10)
+    assert abs(float(lat.quantity("T").double().mean()) - 1.0) < 1e-12
+    assert float(lat.quantity("U").double().abs().max()) < 1e-12
