@@ -35,13 +35,19 @@ def _blocks(_m):
 
 
 def build(outflowconvective=False, outflowneumann=False, avg=False, ibb=False, smag=False, cht=False,
-          name="d3q27q7_cm_cht") -> Model:
-    m = Model(name, dims=3, family="heat", reference="models/heat/d3q27q7_cm_cht",
-              description="D3Q27xD3Q7 conjugate heat transfer (cumulant flow, central-moment heat)")
+          heat_q=7) -> Model:
+    """heat_q = 7: d3q27q7_cm_cht; heat_q = 27: d3q27q27_cm_cht (reference
+    models/heat/d3q27q27_cm_cht/Dynamics.R, same settings/globals/zones, D3Q27 heat set and
+    the CM_HIGHER / CM_HIGHER_PROB / CM_HIGHER_PROB_M_EQ / Cumulants / Cumulants_HIGHER
+    collisions)."""
+    name = f"d3q27q{heat_q}_cm_cht"
+    m = Model(name, dims=3, family="heat", reference=f"models/heat/{name}",
+              description=f"D3Q27xD3Q{heat_q} conjugate heat transfer (cumulant flow, central-moment heat)")
+    HU = U7 if heat_q == 7 else U
     for k in range(27):
         m.add_density(f"f[{k}]", int(U[k, 0]), int(U[k, 1]), int(U[k, 2]), group="f",
                       comment=f"flow LB density F{P[k, 0]}{P[k, 1]}{P[k, 2]}")
-    for i, c in enumerate(U7):
+    for i, c in enumerate(HU):
         m.add_density(f"h[{i}]", int(c[0]), int(c[1]), int(c[2]), group="h", comment=f"heat LB density H{i}")
     S = m.add_setting
     for a in "XYZ":
@@ -95,8 +101,12 @@ def build(outflowconvective=False, outflowneumann=False, avg=False, ibb=False, s
     for n in ("HeaterDirichletTemperatureEQ", "HeaterDirichletTemperatureABB", "HeaterSource",
               "HeaterNeumannHeatFluxCylinder", "HeaterNeumannHeatFluxEast"):
         m.add_node_type(n, "ADDITIONALS_HEAT")
-    m.add_node_type("CM", "COLLISION")
-    m.add_node_type("CM_PROB", "COLLISION")
+    if heat_q == 7:
+        m.add_node_type("CM", "COLLISION")
+        m.add_node_type("CM_PROB", "COLLISION")
+    else:
+        for n in ("CM_HIGHER", "CM_HIGHER_PROB", "CM_HIGHER_PROB_M_EQ", "Cumulants", "Cumulants_HIGHER", "CM"):
+            m.add_node_type(n, "COLLISION")
     S("CylinderCenterX", default=0, comment="X coord of cylinder with imposed heat flux")
     S("CylinderCenterY", default=0, comment="Y coord of cylinder with imposed heat flux")
     S("CylinderCenterX_GH", default=0, comment="X coord of Gaussian Hill")
@@ -110,7 +120,7 @@ def build(outflowconvective=False, outflowneumann=False, avg=False, ibb=False, s
         S("Smag", default=0, comment="Smagorinsky coefficient for SGS modeling")
     m.add_density("U", 0, 0, 0, group="Vel")
     if outflowconvective:
-        for k in range(7):
+        for k in range(heat_q):
             m.add_density(f"hold[{k}]", 0, 0, 0, group="hold", comment=f"heat LB density H{k}")
         for k in range(27):
             m.add_density(f"fold[{k}]", 0, 0, 0, group="fold", comment=f"flow LB density F{k}")
@@ -140,5 +150,5 @@ def build(outflowconvective=False, outflowneumann=False, avg=False, ibb=False, s
     m.options = {"OutFlowConvective": outflowconvective, "OutFlowNeumann": outflowneumann, "AVG": avg,
                  "IBB": ibb, "SMAG": smag, "CHT": cht}
     m.add_codegen(_blocks)
-    m.set_dynamics("heat/d3q27q7_cm_cht.inc")
+    m.set_dynamics(f"heat/{name}.inc")
     return m

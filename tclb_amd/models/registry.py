@@ -137,3 +137,6 @@ for _o in ("OutFlowConvective", "OutFlowNeumann", "AVG", "IBB", "SMAG", "CHT"):
 register("d3q27q7_cm_cht", ".heat.d3q27q7_cm_cht")
 for _o in ("OutFlowConvective", "OutFlowNeumann", "AVG", "IBB", "SMAG", "CHT"):
     register(f"d3q27q7_cm_cht_{_o}", ".heat.d3q27q7_cm_cht", **{_o.lower(): True})
+register("d3q27q27_cm_cht", ".heat.d3q27q7_cm_cht", heat_q=27)
+for _o in ("OutFlowConvective", "OutFlowNeumann", "AVG", "IBB", "SMAG", "CHT"):
+    register(f"d3q27q27_cm_cht_{_o}", ".heat.d3q27q7_cm_cht", heat_q=27, **{_o.lower(): True})

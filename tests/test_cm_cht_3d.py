@@ -25,10 +25,14 @@ def _lat(shape, collision="CM", extra=None, model="d3q27q7_cm_cht", **settings):
     return lat
 
 
-@pytest.mark.parametrize("collision", ["CM", "CM_PROB", "BGK"])
-def test_heat_diffusion(collision):
+Q27_COLLISIONS = ["CM_HIGHER", "CM_HIGHER_PROB", "CM_HIGHER_PROB_M_EQ", "Cumulants", "Cumulants_HIGHER", "CM", "BGK"]
+
+
+@pytest.mark.parametrize("model,collision", [("d3q27q7_cm_cht", c) for c in ("CM", "CM_PROB", "BGK")] +
+                         [("d3q27q27_cm_cht", c) for c in Q27_COLLISIONS])
+def test_heat_diffusion(model, collision):
     nx, k, steps, a = 32, 0.05, 300, 0.05
-    lat = _lat((nx, 2, 2), collision, conductivity=k, InitTemperature=1.0, nu=0.1)
+    lat = _lat((nx, 2, 2), collision, model=model, conductivity=k, InitTemperature=1.0, nu=0.1)
     m = lat.model
     f = lat.fields_interior().clone()
     x = torch.arange(nx, dtype=f.dtype)
@@ -45,9 +49,10 @@ def test_heat_diffusion(collision):
     assert abs(t.mean() - 1.0) < 1e-10
 
 
-def test_boussinesq_acceleration():
+@pytest.mark.parametrize("model,collision", [("d3q27q7_cm_cht", "CM"), ("d3q27q27_cm_cht", "CM_HIGHER")])
+def test_boussinesq_acceleration(model, collision):
     n, g, B, T = 20, 1e-5, 0.05, 12.0
-    lat = _lat((4, 4, 4), InitTemperature=T, GravitationZ=g, BoussinesqCoeff=B, nu=0.1, conductivity=0.1)
+    lat = _lat((4, 4, 4), collision, model=model, InitTemperature=T, GravitationZ=g, BoussinesqCoeff=B, nu=0.1, conductivity=0.1)
     lat.iterate(n)
     uz = lat.quantity("U")[2].double()
     a = g * (1 - B * (T - 10.0))
@@ -56,12 +61,12 @@ def test_boussinesq_acceleration():
     assert float(lat.quantity("U")[:2].double().abs().max()) < 1e-12
 
 
-def _heater_lat(kind, nx=24):
+def _heater_lat(kind, nx=24, model="d3q27q7_cm_cht", collision="CM"):
     """west slab (x = 0, 1) is a heater zone at T = 1; the bulk starts at T = 0"""
-    lat = Lattice("d3q27q7_cm_cht", (nx, 2, 2))
+    lat = Lattice(model, (nx, 2, 2))
     m = lat.model
     zi = lat.zone_index("heater")
-    flags = np.full((lat.NZ, lat.NY, nx), m.node_type("CM").value, dtype=np.uint32)
+    flags = np.full((lat.NZ, lat.NY, nx), m.node_type(collision).value, dtype=np.uint32)
     flags[:, :, :2] |= m.node_type(kind).value | (zi << m.zone_shift)
     if kind == "HeaterDirichletTemperatureABB":
         flags[:, :, :2] |= m.node_type("Wall").value
@@ -73,15 +78,32 @@ def _heater_lat(kind, nx=24):
     return lat
 
 
+@pytest.mark.parametrize("model,collision", [("d3q27q7_cm_cht", "CM"), ("d3q27q27_cm_cht", "CM_HIGHER")])
 @pytest.mark.parametrize("kind", ["HeaterDirichletTemperatureEQ", "HeaterDirichletTemperatureABB"])
-def test_dirichlet_heater(kind):
-    lat = _heater_lat(kind)
+def test_dirichlet_heater(kind, model, collision):
+    lat = _heater_lat(kind, model=model, collision=collision)
     lat.iterate(400)
     t = lat.quantity("T")[0, 0, 0].double().numpy()
     inner = t[2:12]
     assert np.all(np.diff(inner) < 0), inner
     assert 0.0 < inner[-1] < inner[0] < 1.0, inner
     assert lat.globals["HeatSource"] > 0.0
+
+
+def test_neumann_flux_q27_moments():
+    """the east Neumann heater's D3Q27 increment (first, third and fifth order moments
+    along the normal) carries no enthalpy: the HeatSource global stays zero"""
+    lat = Lattice("d3q27q27_cm_cht", (4, 2, 2))
+    m = lat.model
+    zi = lat.zone_index("hot")
+    fl = np.full((lat.NZ, lat.NY, 4), m.node_type("CM_HIGHER").value, dtype=np.uint32)
+    fl[:, :, 0] |= m.node_type("HeaterNeumannHeatFluxEast").value | (zi << m.zone_shift)
+    lat.set_flags(fl)
+    lat.set_setting("InitTemperature", 1.0)
+    lat.set_setting("InitHeatFlux", 0.01, zone="hot")
+    lat.init()
+    lat.iterate(1)
+    assert abs(lat.globals["HeatSource"]) < 1e-12
 
 
 def test_pressure_driven_channel():
@@ -116,11 +138,11 @@ def test_pressure_driven_channel():
     assert 0.0 < t[ny // 2, nx // 2] < 1.0 + 1e-9
 
 
-@pytest.mark.parametrize("variant", ["d3q27q7_cm_cht_OutFlowNeumann", "d3q27q7_cm_cht_OutFlowConvective",
-                                     "d3q27q7_cm_cht_AVG", "d3q27q7_cm_cht_CHT", "d3q27q7_cm_cht_SMAG",
-                                     "d3q27q7_cm_cht_IBB"])
+@pytest.mark.parametrize("variant", [f"d3q27q{q}_cm_cht_{o}" for q in (7, 27) for o in
+                                     ("OutFlowNeumann", "OutFlowConvective", "AVG", "CHT", "SMAG", "IBB")])
 def test_variants_conserve_uniform_state(variant):
-    lat = _lat((6, 4, 4), model=variant, InitTemperature=1.0, nu=0.1, conductivity=0.1)
+    coll = "CM" if "q7_" in variant else "CM_HIGHER"
+    lat = _lat((6, 4, 4), coll, model=variant, InitTemperature=1.0, nu=0.1, conductivity=0.1)
     lat.iterate(10)
     assert abs(float(lat.quantity("T").double().mean()) - 1.0) < 1e-12
     assert float(lat.quantity("U").double().abs().max()) < 1e-12
