@@ -47,8 +47,8 @@ def channel_flags(lat: Lattice) -> np.ndarray:
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=30)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--size", type=int, default=512)
     ap.add_argument("--model", default="d3q27")
     ap.add_argument("--precision", default="double", choices=["double", "float", "mixed"])

@@ -34,6 +34,7 @@ VARIANTS = {
     "nt": ["-DTCLB_NT_LOAD=1", "-DTCLB_NT_STORE=1"],
     "ntld": ["-DTCLB_NT_LOAD=1"],
     "noxs": ["-DTCLB_DEBUG_NO_XSHIFT", "-DTCLB_NT_STORE=1"],   # diagnostic: aligned-x ceiling
+    "xcd": ["-DTCLB_NT_STORE=1", "-DTCLB_XCD_REMAP=1"],        # XCD-contiguous block->tile map
 }
 DEFAULT_VARIANT = os.environ.get("TCLB_VARIANT", "")
 

@@ -66,11 +66,32 @@ __device__ __forceinline__ void block_globals(R* g, double* dst) {
   }
 }
 
+// Block -> tile map.  Workgroups are dealt round-robin over the 8 XCDs (b and b+8 share
+// an L2; MI355X_MICROARCH.md, Workgroup dispatch).  With TCLB_XCD_REMAP the linear block
+// id b is remapped so that XCD (b % 8) owns one contiguous 1/8 of the tiles (a z-range):
+// x-neighbouring tiles, which share the partial 128-B lines of the x-shifted pull loads,
+// and y/z-neighbouring tiles of stencil stages then meet in the same L2.  Speed only:
+// any placement gives the same result.
+#ifndef TCLB_XCD_REMAP
+#define TCLB_XCD_REMAP 0
+#endif
+__device__ __forceinline__ uint3 tile_id() {
+#if TCLB_XCD_REMAP
+  const unsigned gx = gridDim.x, gy = gridDim.y, T = gridDim.x * gridDim.y * gridDim.z;
+  unsigned b = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
+  if ((T & 7u) == 0u) b = (b & 7u) * (T >> 3) + (b >> 3);
+  return make_uint3(b % gx, (b / gx) % gy, b / (gx * gy));
+#else
+  return make_uint3(blockIdx.x, blockIdx.y, blockIdx.z);
+#endif
+}
+
 template <class Model, class R, class S, int STG, bool GLOB>
 __global__ void __launch_bounds__(256) k_stage(const Launch L) {
-  const int x = L.xlo + (int)(blockIdx.x * blockDim.x + threadIdx.x);
-  const int y = L.ylo + (int)(blockIdx.y * blockDim.y + threadIdx.y);
-  const int z = L.zlo + (int)blockIdx.z;
+  const uint3 t = tile_id();
+  const int x = L.xlo + (int)(t.x * blockDim.x + threadIdx.x);
+  const int y = L.ylo + (int)(t.y * blockDim.y + threadIdx.y);
+  const int z = L.zlo + (int)t.z;
   constexpr int NG = GLOB ? Model::NGLOBALS_ : 1;
   R g[NG];
 #pragma unroll

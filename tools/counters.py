@@ -1,0 +1,129 @@
+#!/usr/bin/env python3
+"""Hardware-counter profile of a command: per-kernel time, real HBM bytes, L2 hit rate,
+LDS bank conflicts and wave statistics from rocprofv3 PMC passes.
+
+    python tools/counters.py --tag d3q27_512 --nodes 134217728 -- python3 bench.py --steps 5 --warmup 1
+
+Runs ONE kernel-trace pass and one rocprofv3 ``--pmc`` pass per counter group (each
+group fits the gfx950 per-pass slot limits: TCC 4, SQ 8, GRBM 2), every pass under its
+own hard time limit, then joins the per-dispatch rows by kernel name and prints a CSV
+(and writes ``<outdir>/<tag>_counters.csv``):
+
+    kernel, calls, mean_ms, fetch_MB, write_MB, hbm_TBps, B_per_node, l2_hit, lds_conflict_per_wave, ...
+
+``fetch_MB`` is reported raw (FETCH_SIZE KiB) and corrected (x2: on gfx950 FETCH_SIZE
+counts half of the bytes of wide coalesced streaming reads, MI355X_MICROARCH.md §HBM);
+``--calib`` adds a torch device copy of a known byte count to the same passes so the
+correction factor of this access pattern can be read off directly.
+"""
+from __future__ import annotations
+
+import argparse
+import csv
+import glob
+import os
+import subprocess
+import sys
+from collections import defaultdict
+
+PASSES = [
+    ["FETCH_SIZE"],
+    ["WRITE_SIZE", "TCC_HIT_sum", "TCC_MISS_sum"],
+    ["SQ_WAVES", "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES", "SQ_INSTS_VALU", "SQ_INSTS_LDS",
+     "SQ_LDS_BANK_CONFLICT", "SQ_WAIT_ANY", "SQ_ACTIVE_INST_ANY", "GRBM_GUI_ACTIVE", "GRBM_COUNT"],
+]
+
+
+def _rows(pattern):
+    out = []
+    for p in glob.glob(pattern, recursive=True):
+        with open(p, newline="") as f:
+            out += list(csv.DictReader(f))
+    return out
+
+
+def _short(name: str) -> str:
+    name = name.replace(",", ";")
+    return name if len(name) < 160 else name[:157] + "..."
+
+
+def run_pass(outdir, tag, k, extra, cmd, timeout):
+    d = os.path.join(outdir, f"{tag}_p{k}")
+    os.makedirs(d, exist_ok=True)
+    full = ["timeout", "-s", "KILL", str(timeout), "rocprofv3", *extra, "-f", "csv", "-d", d, "-o", "run", "--", *cmd]
+    print("[counters]", " ".join(full), flush=True)
+    r = subprocess.run(full, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    with open(os.path.join(d, "log.txt"), "w") as f:
+        f.write(r.stdout)
+    if r.returncode != 0:
+        print(r.stdout[-3000:], flush=True)
+        raise SystemExit(f"pass {k} failed with code {r.returncode}")
+    return d
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--tag", required=True)
+    ap.add_argument("--outdir", default="gpurun_out/counters")
+    ap.add_argument("--nodes", type=float, default=0.0, help="lattice nodes per dispatch (for B/node)")
+    ap.add_argument("--timeout", type=int, default=120)
+    ap.add_argument("--passes", default="0,1,2")
+    ap.add_argument("cmd", nargs=argparse.REMAINDER)
+    a = ap.parse_args()
+    cmd = a.cmd[1:] if a.cmd and a.cmd[0] == "--" else a.cmd
+    if not cmd:
+        ap.error("no command")
+    os.makedirs(a.outdir, exist_ok=True)
+    # kernel trace: durations and resources
+    d = run_pass(a.outdir, a.tag, "t", ["--kernel-trace"], cmd, a.timeout)
+    kt = _rows(os.path.join(d, "**", "*kernel_trace.csv"))
+    stats = defaultdict(lambda: {"calls": 0, "ns": 0, "vgpr": "", "sgpr": "", "lds": "", "scratch": ""})
+    for r in kt:
+        s = stats[_short(r["Kernel_Name"])]
+        s["calls"] += 1
+        s["ns"] += int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+        s["vgpr"] = r.get("VGPR_Count", r.get("Arch_VGPR_Count", ""))
+        s["sgpr"] = r.get("SGPR_Count", "")
+        s["lds"] = r.get("Group_Segment_Size", r.get("LDS_Block_Size", ""))
+        s["scratch"] = r.get("Private_Segment_Size", r.get("Scratch_Size", ""))
+    ctr = defaultdict(lambda: defaultdict(list))
+    for k in (int(v) for v in a.passes.split(",") if v != ""):
+        d = run_pass(a.outdir, a.tag, k, ["--pmc", *PASSES[k]], cmd, a.timeout)
+        for r in _rows(os.path.join(d, "**", "*counter_collection.csv")):
+            ctr[_short(r["Kernel_Name"])][r["Counter_Name"]].append(float(r["Counter_Value"]))
+
+    def mean(name, c):
+        v = ctr[name].get(c)
+        return sum(v) / len(v) if v else float("nan")
+
+    cols = ["kernel", "calls", "mean_ms", "fetch_MB_raw", "fetch_MB_x2", "write_MB", "hbm_TBps_x2",
+            "B_per_node_x2", "l2_hit", "valu_per_wave", "lds_insts_per_wave", "lds_conflict_cycles_per_wave",
+            "wait_any_frac", "eff_clock_GHz", "vgpr", "sgpr", "lds_B", "scratch_B"]
+    lines = [",".join(cols)]
+    for name, s in sorted(stats.items(), key=lambda kv: -kv[1]["ns"]):
+        ms = s["ns"] / s["calls"] / 1e6
+        fetch = mean(name, "FETCH_SIZE") * 1024 / 1e6
+        write = mean(name, "WRITE_SIZE") * 1024 / 1e6
+        hit, miss = mean(name, "TCC_HIT_sum"), mean(name, "TCC_MISS_sum")
+        waves = mean(name, "SQ_WAVES")
+        tot = 2 * fetch + write
+        tbps = tot * 1e6 / (ms * 1e-3) / 1e12 if ms > 0 else float("nan")
+        bpn = tot * 1e6 / a.nodes if a.nodes else float("nan")
+        wc = mean(name, "SQ_WAVE_CYCLES")
+        clk = mean(name, "GRBM_GUI_ACTIVE") / 8 / (ms * 1e-3) / 1e9 if ms > 0 else float("nan")
+        row = [name, s["calls"], f"{ms:.4f}", f"{fetch:.2f}", f"{2 * fetch:.2f}", f"{write:.2f}", f"{tbps:.3f}",
+               f"{bpn:.1f}", f"{hit / (hit + miss):.3f}" if hit == hit and hit + miss > 0 else "nan",
+               f"{mean(name, 'SQ_INSTS_VALU') / waves:.1f}" if waves == waves and waves else "nan",
+               f"{mean(name, 'SQ_INSTS_LDS') / waves:.2f}" if waves == waves and waves else "nan",
+               f"{mean(name, 'SQ_LDS_BANK_CONFLICT') / waves:.2f}" if waves == waves and waves else "nan",
+               f"{mean(name, 'SQ_WAIT_ANY') / wc:.3f}" if wc == wc and wc else "nan",
+               f"{clk:.2f}", s["vgpr"], s["sgpr"], s["lds"], s["scratch"]]
+        lines.append(",".join(str(v) for v in row))
+    text = "\n".join(lines)
+    print(text)
+    with open(os.path.join(a.outdir, f"{a.tag}_counters.csv"), "w") as f:
+        f.write(text + "\n")
+
+
+if __name__ == "__main__":
+    sys.exit(main())

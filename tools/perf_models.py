@@ -21,14 +21,17 @@ def main():
     ap.add_argument("--n2", type=int, default=4096)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--precision", default="double")
+    ap.add_argument("--variants", default="", help="comma list of HIP build variants to A/B (interleaved)")
+    ap.add_argument("--rounds", type=int, default=1)
     a = ap.parse_args()
+    variants = a.variants.split(",") if a.variants else [None]
     names = a.models.split(",") if a.models else registry.names()
     dev = torch.device("cuda", 0)
-    for name in names:
+    for name, variant, rnd in [(n, v, r) for n in names for r in range(a.rounds) for v in variants]:
         m = registry.get(name)
         shape = (a.n3, a.n3, a.n3) if m.dims == 3 else (a.n2, a.n2, 1)
         try:
-            lat = Lattice(name, shape, device=dev, precision=a.precision)
+            lat = Lattice(name, shape, device=dev, precision=a.precision, variant=variant)
             coll = next((n.value for n in m.node_types if n.group == "COLLISION"), 0)
             lat.set_flags(np.full((lat.NZ, lat.NY, shape[0]), coll, dtype=np.uint32))
             lat.init()
@@ -41,7 +44,7 @@ def main():
             es = 8 if a.precision == "double" else 4
             nodes = shape[0] * shape[1] * shape[2]
             bpn = 2 * lat.nf * es + lat.flags.element_size()
-            print(json.dumps({"model": name, "shape": shape, "fields": lat.nf, "stages": len(m.stages),
+            print(json.dumps({"model": name, "variant": variant, "round": rnd, "shape": shape, "fields": lat.nf, "stages": len(m.stages),
                               "ms": round(dt * 1e3, 3), "MLUPS": round(nodes / dt / 1e6, 1),
                               "GBps_meter": round(nodes * bpn / dt / 1e9, 1)}), flush=True)
             del lat

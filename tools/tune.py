@@ -64,7 +64,7 @@ def main():
                 lat.iterate(a.steps, glob_last=False)
                 torch.cuda.synchronize()
                 dt = (time.perf_counter() - t) / a.steps
-                key = f"{v or 'plain'}/{blk}"
+                key = f"{v or 'default'}/{blk}"
                 res.setdefault(key, []).append(dt)
                 print(json.dumps({"round": r, "cfg": key, "ms": round(dt * 1e3, 3),
                                   "MLUPS": round(n ** 3 / dt / 1e6, 1),
