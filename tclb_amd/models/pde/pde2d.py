@@ -40,9 +40,11 @@ def build_advection_diffusion(fields: bool = False) -> Model:
     return m
 
 
-def build_wave() -> Model:
+def build_wave(autosym: int = 0) -> Model:
+    """reference OPT="autosym": symmetry node types mirror the u/v stencil reads"""
     m = Model("wave2D", dims=2, family="PDE", reference="models/PDE/wave2D",
               description="explicit damped wave equation")
+    m.options["autosym"] = autosym
     _common(m, ["u", "v"])
     m.add_quantity("U")
     m.add_setting("Speed")

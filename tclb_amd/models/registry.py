@@ -1,35 +1,129 @@
 """Model registry (replaces the reference's conf.mk discovery, src/models.R:20-90).
 
-Every model is a Python module exposing ``build() -> Model``; variants (the reference's
-``OPT=`` option products, e.g. ``d2q9_bc_autosym``) are registered as separate entries
-with option dictionaries."""
+Every model is a Python module exposing ``build(**options) -> Model``.  Two kinds of
+entries:
+
+* ``register(name, module, builder, **kwargs)`` — one named variant; these form the
+  default catalog that ``tclb_amd.build`` compiles up front (``names()``).
+* ``family(base, module, formula, ...)`` — the reference's ``OPT=`` option formula of a
+  model (models/**/conf.mk).  Every product of the formula (``options.expand``) is a
+  valid model name, resolved lazily by ``get()`` and compiled on first use
+  (``all_variants()`` lists them).  Option names map to builder keyword arguments
+  (default: the lower-cased option name = True; ``autosym`` = its level 1/2).  A
+  product whose options the builder does not take is reported by ``variant_status``
+  and raises ``NotImplementedError`` in ``get``.
+"""
 from __future__ import annotations
 
 import importlib
-from typing import Callable, Dict, List, Optional
+import inspect
+from typing import Callable, Dict, List, Optional, Tuple
 
 from .dsl import Model
+from .options import expand, variant_options
 
-# name -> (module, kwargs)
+# name -> (module, builder, kwargs)
 _MODELS: Dict[str, tuple] = {}
+# base -> (module, builder, formula, optmap, fixed kwargs)
+_FAMILIES: Dict[str, tuple] = {}
 
 
 def register(name: str, module: str, builder: str = "build", **kwargs):
     _MODELS[name] = (module, builder, kwargs)
 
 
+def family(base: str, module: str, formula: str, builder: str = "build",
+           optmap: Optional[Dict[str, Callable[[int], dict]]] = None, **fixed):
+    _FAMILIES[base] = (module, builder, formula, optmap or {}, fixed)
+
+
 def names() -> List[str]:
+    """the default catalog (compiled by ``python -m tclb_amd.build``)"""
     return sorted(_MODELS)
+
+
+def families() -> Dict[str, str]:
+    return {b: f[2] for b, f in _FAMILIES.items()}
+
+
+def all_variants() -> List[str]:
+    """every name of every option product (the reference's full variant table)"""
+    out = set(_MODELS)
+    for base, (_, _, formula, _, _) in _FAMILIES.items():
+        out.update(v.name for v in expand(base, formula))
+    return sorted(out)
+
+
+def _kwargs_for(base: str, opts: Dict[str, int]) -> dict:
+    module, builder, formula, optmap, fixed = _FAMILIES[base]
+    kw = dict(fixed)
+    for o, lvl in opts.items():
+        if o in optmap:
+            kw.update(optmap[o](lvl))
+        elif o == "autosym":
+            kw["autosym"] = lvl
+        else:
+            kw[o.lower()] = True
+    return kw
+
+
+def _resolve(name: str) -> Optional[Tuple[str, str, dict]]:
+    """(module, builder, kwargs) of a family variant name, or None"""
+    for base in sorted(_FAMILIES, key=len, reverse=True):
+        if name != base and not name.startswith(base + "_"):
+            continue
+        module, builder, formula, _, _ = _FAMILIES[base]
+        try:
+            opts = variant_options(base, formula, name)
+        except KeyError:
+            continue
+        return module, builder, _kwargs_for(base, opts)
+    return None
+
+
+def _missing_kwargs(module: str, builder: str, kw: dict) -> List[str]:
+    m = importlib.import_module(module, package=__package__)
+    sig = inspect.signature(getattr(m, builder))
+    if any(p.kind == p.VAR_KEYWORD for p in sig.parameters.values()):
+        return []
+    return [k for k in kw if k not in sig.parameters]
+
+
+def variant_status(name: str) -> str:
+    """'ok', 'unknown', or 'not implemented: <builder options missing>'"""
+    if name in _MODELS:
+        return "ok"
+    r = _resolve(name)
+    if r is None:
+        return "unknown"
+    try:
+        miss = _missing_kwargs(*r)
+    except ModuleNotFoundError:
+        return "not implemented: model module " + r[0]
+    return "ok" if not miss else "not implemented: " + ", ".join(miss)
 
 
 _cache: Dict[str, Model] = {}
 
 
+def exists(name: str) -> bool:
+    return name in _MODELS or _resolve(name) is not None
+
+
 def get(name: str) -> Model:
-    if name not in _MODELS:
-        raise KeyError(f"unknown model '{name}'; known: {', '.join(names())}")
     if name not in _cache:
-        mod, builder, kw = _MODELS[name]
+        if name in _MODELS:
+            mod, builder, kw = _MODELS[name]
+        else:
+            r = _resolve(name)
+            if r is None:
+                raise KeyError(f"unknown model '{name}'; known: {', '.join(names())} "
+                               f"(+ option products of {', '.join(sorted(_FAMILIES))})")
+            mod, builder, kw = r
+            miss = _missing_kwargs(mod, builder, kw)
+            if miss:
+                raise NotImplementedError(f"model variant '{name}' needs builder options not implemented: "
+                                          f"{', '.join(miss)}")
         m = importlib.import_module(mod, package=__package__)
         model = getattr(m, builder)(**kw)
         if model.name != name:
@@ -140,3 +234,41 @@ for _o in ("OutFlowConvective", "OutFlowNeumann", "AVG", "IBB", "SMAG", "CHT"):
 register("d3q27q27_cm_cht", ".heat.d3q27q7_cm_cht", heat_q=27)
 for _o in ("OutFlowConvective", "OutFlowNeumann", "AVG", "IBB", "SMAG", "CHT"):
     register(f"d3q27q27_cm_cht_{_o}", ".heat.d3q27q7_cm_cht", heat_q=27, **{_o.lower(): True})
+
+
+# ---- option formulas of the reference (models/**/conf.mk OPT=) --------------------
+def _set(key, value):
+    return lambda lvl: {key: value}
+
+
+family("d2q9", ".flow.d2q9", "bc*autosym")
+family("d2q9_par", ".flow.d2q9", "BC", par=True)
+family("d2q9_part", ".flow.d2q9", "BC", part=True)
+family("d3q27_cumulant", ".flow.d3q27_cumulant", "AVG*IB*SMAG")
+family("d3q27_cumulant_part", ".flow.d3q27_cumulant", "AVG*IB*SMAG", part=True)
+family("auto", ".flow.auto", "d3q19*part*(TRT+BGK+WMRT)*FMT*HiOrd*autosym",
+       optmap={"d3q19": _set("q19", True), "TRT": _set("coll", "TRT"), "BGK": _set("coll", "BGK"),
+               "WMRT": _set("coll", "WMRT"), "FMT": _set("fmt", True), "HiOrd": _set("hiord", True)})
+family("d3q27_PSM", ".particles.d3q27_psm", "MS*KL*TRT*(NEBB+SUP+(NEBB+SEP):singlekernel)")
+family("d3q27_viscoplastic", ".nonnewtonian.d3q27_viscoplastic", "OutFlow")
+family("d3q27_kl", ".nonnewtonian.d3q27_kl", "OutFlow")
+family("advection_diffusion2D", ".pde.pde2d", "fields", builder="build_advection_diffusion")
+family("wave2D", ".pde.pde2d", "autosym", builder="build_wave")
+_RDS = ("AllenCahn", "SIR_ModifiedPeng", "SIR_SimpleLaplace", "SimpleDiffusion", "LinearReaction")
+_RDI = {"Trapezoidal": "Trapezoid", "Midpoint": "Midpoint", "Heun": "Heun", "Euler": "Euler"}
+family("d2q9_reaction_diffusion_system", ".reaction.d2q9_reaction_diffusion_system",
+       "(AllenCahn+SIR_ModifiedPeng+SIR_SimpleLaplace+SimpleDiffusion+LinearReaction)*(Trapezoidal+Midpoint+Heun+Euler)-1",
+       optmap={**{s_: _set("system", s_) for s_ in _RDS}, **{k: _set("integrator", v) for k, v in _RDI.items()}})
+family("d2q9_AllenCahn_SourceTerm_SOI", ".reaction.d2q9_AllenCahn_SourceTerm_SOI", "ExpotentialDecay")
+family("d3q27_pf_velocity", ".multiphase.d3q27_pf_velocity",
+       "(q27 + OutFlow  + BGK + thermo*planarBenchmark)*autosym*geometric*staircaseimp*isograd*tprec",
+       optmap={"planarBenchmark": _set("planarbenchmark", True)})
+family("d2q9_pf", ".multiphase.d2q9_pf", "no_bc+fd")
+family("d2q9_pf_velocity", ".multiphase.d2q9_pf_velocity", "(GF+RT+Outflow+GuoCM+debug+BGK+CM)*autosym")
+family("d2q9_scmp", ".multiphase.d2q9_scmp",
+       "(LycettLuo+Kupershtokh)*VirtualRhoWBC*ViscositySmooth*(TRT+BGK+WMRT+CUM)*FMT*HiOrd-1")
+family("d2q9_csf", ".multiphase.d2q9_csf", "(bc+bcinit)*noflow*weno*viscstep*cumulant")
+family("d2q9q9_cm_cht", ".heat.d2q9q9_cm_cht", "OutFlowConvective*OutFlowNeumann*AVG*IBB*SMAG*CHT")
+family("d3q27q7_cm_cht", ".heat.d3q27q7_cm_cht", "OutFlowConvective*OutFlowNeumann*AVG*IBB*SMAG*CHT")
+family("d3q27q27_cm_cht", ".heat.d3q27q7_cm_cht", "OutFlowConvective*OutFlowNeumann*AVG*IBB*SMAG*CHT", heat_q=27)
+family("d3q27_tePSM_per", ".heat.d3q27_tepsm_per", "(NEBB+SUP)*Isothermal")
