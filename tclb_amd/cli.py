@@ -37,9 +37,8 @@ def main(argv=None):
     from . import handlers  # noqa: F401
     from .parallel.comm import init_distributed_from_env
     from .solver import Solver
-    from .utils.xpath import apply_edits, strip_comments
-    tree = ET.parse(a.config)
-    root = tree.getroot()
+    from .utils.xpath import apply_edits, load_case
+    root = load_case(a.config)
     root, exit_now = apply_edits(root, a.edits)
     if exit_now:
         return 0

@@ -4,8 +4,12 @@ pressure-evolution LBM for high-density-ratio two-phase flow: hydrodynamics on D
 with ``q27``).  Two distribution sets g (27) and h (15/27) + macroscopic/wall fields.
 
 Reference: models/multiphase/d3q27_pf_velocity/{Dynamics.R, model.R, Dynamics.c.Rt,
-Boundary.c.Rt}.  Implemented option subset: base, ``q27``, ``BGK`` (OutFlow, thermo,
-geometric, staircaseimp, isograd, tprec are not built in this round).
+Boundary.c.Rt, thermocapillary.R, thermo.c.Rt}.  Implemented options: ``q27``, ``BGK``,
+``OutFlow`` (Neumann / convective E,W outflow with the gold/hold history sets),
+``thermo`` (temperature field by explicit RK4 with phase-dependent conductivity and heat
+capacity; surface tension sigma(T) enters the chemical potential and a Marangoni force),
+``planarBenchmark`` (heated-wall layered benchmark initialisation, with ``thermo``) and
+``autosym`` (1/2); geometric, staircaseimp, isograd and tprec are not built yet.
 
 Build-time derivations (sympy, replacing the reference's R polynomial algebra):
 * the 27x27 moment matrix M factorises as M = C . Mraw, Mraw the raw-monomial
@@ -61,7 +65,8 @@ def _bounce(U):
     return [idx[tuple((-np.array(r)).tolist())] for r in U.tolist()]
 
 
-def build(q27: bool = False, bgk: bool = False) -> Model:
+def build(q27: bool = False, bgk: bool = False, thermo: bool = False, planarbenchmark: bool = False,
+          outflow: bool = False, autosym: int = 0) -> Model:
     m = Model("d3q27_pf_velocity", dims=3, family="multiphase", reference="models/multiphase/d3q27_pf_velocity",
               description="phase-field (D3Q15/D3Q27 h) + velocity-based hydrodynamics (D3Q27 g), "
                           "weighted-MRT, high density ratio")
@@ -87,6 +92,27 @@ def build(q27: bool = False, bgk: bool = False) -> Model:
     save_iteration = ["g", "h", "Vel", "nw", "solid_boundary"]
     load_iteration = ["g", "h", "Vel", "nw", "solid_boundary"]
     load_phase = ["g", "h", "Vel", "nw", "solid_boundary"]
+    if outflow:
+        # Dynamics.R:65-79 + lattice.R:63-66: every density readable one node east/west of
+        # its pull location (Neumann / convective outflow), U readable at x+-1, and the
+        # previous post-collision populations (gold/hold) carried for the convective BC
+        for d in list(m.densities):
+            m.add_field(d.field.name, dx=-d.dx - 1, dy=-d.dy, dz=-d.dz)
+            m.add_field(d.field.name, dx=-d.dx + 1, dy=-d.dy, dz=-d.dz)
+        m.add_field("U", dx=(-1, 1))
+        for i in range(27):
+            m.add_density(f"gold[{i}]", 0, 0, 0, group="gold")
+        for i in range(Qh):
+            m.add_density(f"hold[{i}]", 0, 0, 0, group="hold")
+        save_initial += ["gold", "hold"]
+        save_iteration += ["gold", "hold"]
+        load_iteration += ["gold", "hold"]
+        load_phase += ["gold", "hold"]
+    if thermo:
+        _thermo_declarations(m, planarbenchmark)
+        save_initial_PF = save_initial_PF + ["Thermal"]
+        save_iteration += ["Thermal"]
+        load_iteration += ["Thermal"]
     m.add_stage("PhaseInit", "Init", save_fields=save_initial_PF)
     m.add_stage("BaseInit", "Init_distributions", save_fields=save_initial)
     m.add_stage("calcPhase", "calcPhaseF", save_fields=["PhaseF"], load_densities=load_phase)
@@ -96,10 +122,29 @@ def build(q27: bool = False, bgk: bool = False) -> Model:
     m.add_stage("calcWall", "calcWallPhase", save_fields=["PhaseF"], load_densities=["nw", "solid_boundary"])
     m.add_stage("calcWallPhase_correction", "calcWallPhase_correction", save_fields=["PhaseF"],
                 load_densities=["nw", "solid_boundary"])
-    m.add_action("Iteration", ["BaseIter", "calcPhase", "calcWall", "calcWallPhase_correction"])
-    m.add_action("Init", ["PhaseInit", "WallInit", "calcWall", "calcWallPhase_correction", "BaseInit"])
-    m.add_action("InitFields", ["InitFromFieldsStage", "WallInit", "calcWall", "calcWallPhase_correction",
-                                "BaseInit"])
+    if thermo:
+        # Dynamics.R:124-134, 142-147 (explicit RK4 of the energy equation)
+        T3 = ["Temp", "Cond", "SurfaceTension"]
+        m.add_stage("CopyDistributions", "TempCopy", save_fields=["g", "h", "Vel", "nw", "PF", "Thermal"])
+        m.add_stage("CopyThermal", "ThermalCopy", save_fields=T3, load_densities=T3)
+        m.add_stage("RK_1", "TempUpdate1", save_fields=["RK1"], load_densities=["U", "V", "W", "Cond", "Temp"])
+        m.add_stage("RK_2", "TempUpdate2", save_fields=["RK2"],
+                    load_densities=["U", "V", "W", "RK1", "Cond", "Temp"])
+        m.add_stage("RK_3", "TempUpdate3", save_fields=["RK3"],
+                    load_densities=["U", "V", "W", "RK1", "RK2", "Cond", "Temp"])
+        m.add_stage("RK_4", "TempUpdate4", save_fields=["Temp", "SurfaceTension"],
+                    load_densities=["U", "V", "W", "RK1", "RK2", "RK3", "Cond", "Temp"])
+        m.add_stage("NonLocalTemp", "BoundUpdate", save_fields=["Temp", "SurfaceTension"], load_densities=["Temp"])
+        rk = ["RK_1", "RK_2", "RK_3", "RK_4", "NonLocalTemp"]
+        m.add_action("TempToSteadyState", ["CopyDistributions"] + rk)
+        m.add_action("Iteration", ["BaseIter", "calcPhase", "calcWall"] + rk)
+        m.add_action("IterationConstantTemp", ["BaseIter", "calcPhase", "calcWall", "CopyThermal"])
+        m.add_action("Init", ["PhaseInit", "WallInit", "calcWall", "BaseInit"])
+    else:
+        m.add_action("Iteration", ["BaseIter", "calcPhase", "calcWall", "calcWallPhase_correction"])
+        m.add_action("Init", ["PhaseInit", "WallInit", "calcWall", "calcWallPhase_correction", "BaseInit"])
+        m.add_action("InitFields", ["InitFromFieldsStage", "WallInit", "calcWall", "calcWallPhase_correction",
+                                    "BaseInit"])
     # ---- quantities
     m.add_quantity("Rho", unit="kg/m3")
     m.add_quantity("PhaseField", unit="1")
@@ -180,6 +225,9 @@ def build(q27: bool = False, bgk: bool = False) -> Model:
         m.add_node_type(n, "BOUNDARY")
     m.add_node_type("BGK", "COLLISION")
     m.add_node_type("MRT", "COLLISION")
+    if outflow:
+        for n in ("ENeumann", "WNeumann", "EConvect", "WConvect"):
+            m.add_node_type(n, "BOUNDARY")
     for g, u in [("PressureLoss", "1mPa"), ("OutletFlux", "1m2/s"), ("InletFlux", "1m2/s"),
                  ("TotalDensity", "1kg/m3"), ("KineticEnergy", "J"), ("GasTotalVelocity", "m/s"),
                  ("GasTotalVelocityX", "m/s"), ("GasTotalVelocityY", "m/s"), ("GasTotalVelocityZ", "m/s"),
@@ -188,12 +236,59 @@ def build(q27: bool = False, bgk: bool = False) -> Model:
                  ("NumSpecialPoints", "1"), ("NumWallBoundaryPoints", "1"), ("NumBoundaryPoints", "1"),
                  ("LiqTotalPhase", "1"), ("FluxNodeCount", "1"), ("FluxX", "1"), ("FluxY", "1"), ("FluxZ", "1")]:
         m.add_global(g, unit=u)
-    m.options = {"q27": q27, "BGK": bgk, "OutFlow": False, "thermo": False, "planarBenchmark": False,
-                 "autosym": False, "geometric": False, "staircaseimp": False, "isograd": False, "tprec": False}
+    m.options = {"q27": q27, "BGK": bgk, "OutFlow": outflow, "thermo": thermo,
+                 "planarBenchmark": planarbenchmark, "autosym": autosym, "geometric": False,
+                 "staircaseimp": False, "isograd": False, "tprec": False}
     m.defines["hPops"] = str(Qh)
     m.add_codegen(lambda _m: codegen(Qh))
+    m.add_codegen(_field_index_block)
     m.set_dynamics("multiphase/d3q27_pf_velocity.inc")
     return m
+
+
+def _field_index_block(m: Model) -> str:
+    """field indices of the first g / h / gold / hold population (runtime-indexed reads)"""
+    out = []
+    for arr in ("g", "h", "gold", "hold"):
+        idx = [i for i, f in enumerate(m.fields) if f.array == arr]
+        if idx:
+            assert idx == list(range(idx[0], idx[0] + len(idx)))
+            out.append(f"  static constexpr int FI_{arr.upper()}0 = {idx[0]};")
+    return "\n".join(out)
+
+
+def _thermo_declarations(m: Model, planar: bool):
+    """thermocapillary.R (sourced by Dynamics.R:112-118 before the stages)"""
+    for n in ("Temp", "Cond", "SurfaceTension"):
+        m.add_density(n, 0, 0, 0, group="Thermal")
+    for n in ("Temp", "Cond", "SurfaceTension"):
+        m.add_field(n, stencil3d=1, group="Thermal")
+    m.add_quantity("T", unit="K")
+    m.add_quantity("ST", unit="N/m")
+    S = m.add_setting
+    S("surfPower", default=1, comment="Use for parabolic representation of surface tension")
+    S("sigma_T", comment="Derivative describing how surface tension changes with temp unit=[N/m2]")
+    S("sigma_TT", comment="Derivative describing how surface tension changes with temp unit=[N/m3]")
+    S("T_ref", comment="Reference temperature at which sigma is set unit=[K]")
+    S("T_init", zonal=True, comment="Initial temperature field unit=[K]")
+    S("cp_h", comment="specific heat for heavy phase unit=[J/kg/K]")
+    S("cp_l", comment="specific heat for light phase unit=[J/kg/K]")
+    S("k_h", comment="thermal conductivity for heavy phase unit=[W/m/K]")
+    S("k_l", comment="thermal conductivity for light phase unit=[W/m/K]")
+    S("dT", comment="Application of vertical temp gradient to speed up initialisation unit=[K]")
+    S("dTx", default=0, comment="Application of horizontal temp gradient to speed up initialisation unit=[K]")
+    S("stabiliser", default=1, comment="If not solving flow field, can adjust temperature timestep")
+    m.add_global("TempChange")
+    if planar:
+        for n, v in (("T_c", 10), ("T_h", 20), ("T_0", 4), ("myL", 100), ("MIDPOINT", 51), ("PLUSMINUS", 1)):
+            S(n, default=v)
+        m.add_node_type("BWall", "ADDITIONALS")
+        m.add_node_type("TWall", "ADDITIONALS")
+    for n in ("RK1", "RK2", "RK3"):
+        m.add_density(n, 0, 0, 0, group="Thermal")
+        m.add_field(n, stencil3d=1, group="Thermal")
+    m.add_node_type("ConstantTemp", "ADDITIONALS")
+    m.add_node_type("EAdiabatic", "ADDITIONALS")
 
 
 def codegen(Qh: int) -> str:

@@ -161,3 +161,24 @@ def rewrite_deprecated_params(root):
     if count:
         root.set("permissive", "true")
     return count
+
+
+def load_case(path: str) -> ET.Element:
+    """Parse a case file the way pugixml accepts it (reference src/main.cpp:238-262):
+    comments or blank text before the ``<?xml ...?>`` declaration are dropped (several
+    reference cases start with ``<!-- To be used with <model> -->``), and a byte-order
+    mark is ignored."""
+    with open(path, "rb") as f:
+        raw = f.read()
+    text = raw.decode("utf-8-sig", errors="replace")
+    k = text.find("<?xml")
+    if k > 0:
+        head = text[:k]
+        # only comments / whitespace may precede the declaration
+        import re
+        if re.sub(r"<!--.*?-->", "", head, flags=re.S).strip() == "":
+            text = text[k:]
+    try:
+        return ET.fromstring(text)
+    except ET.ParseError as e:
+        raise XPathError(f"cannot parse case file {path}: {e}") from None
