@@ -9,8 +9,8 @@ import numpy as np
 import sympy as sp
 
 from ..dsl import Model
-from ...emit.blocks import dense_transform, exprs_function
-from ...emit.symbolic import mrt_eq
+from ...emit.blocks import dense_transform, exprs_function, tensor_raw_transform
+from ...emit.symbolic import mrt_eq, poly_matrix
 
 CV = (0, 1, -1)
 
@@ -24,7 +24,44 @@ def lattice(q19: bool):
     return P, U
 
 
-def build(q19: bool = False, part: bool = False, coll: str = "MRT") -> Model:
+def wmrt_matrix(raw) -> sp.Matrix:
+    """WMRT basis of the reference (Dynamics.c.Rt:43-67): A[monomial, moment] holds the
+    coefficients of the order-12 raw equilibrium moments as polynomials in (rho, J);
+    R = qr.R(A) with rows scaled to a unit diagonal; M = mat . R^-1.  R is computed by exact
+    Gram-Schmidt: R[i, j] = <v_i, a_j> / <v_i, v_i> (v_i the orthogonalised columns),
+    which equals qr.R(A)[i, j] / qr.R(A)[i, i] for a full-rank A (no pivoting)."""
+    Req = raw.Req
+    monos = []
+    coef = []
+    for e in Req:
+        d = sp.expand(e).as_coefficients_dict()
+        coef.append(d)
+        for mono in d:
+            if mono not in monos:
+                monos.append(mono)
+    Q = len(Req)
+    A = sp.Matrix(len(monos), Q, lambda r, c: coef[c].get(monos[r], 0))
+    if A.shape[0] > Q or A.rank() < Q:
+        raise ValueError("WMRT: equilibrium coefficient matrix is not of full column rank")
+    R = sp.eye(Q)
+    V = []
+    for j in range(Q):
+        v = A[:, j]
+        for i, vi in enumerate(V):
+            v = v - vi * ((vi.T * A[:, j])[0] / (vi.T * vi)[0])
+        V.append(v)
+    for i in range(Q):
+        nrm = (V[i].T * V[i])[0]
+        for j in range(i, Q):
+            R[i, j] = (V[i].T * A[:, j])[0] / nrm
+    return raw.mat * R.inv()
+
+
+def build(q19: bool = False, part: bool = False, coll: str = "MRT", fmt: bool = False, hiord: bool = False,
+          autosym: int = 0) -> Model:
+    """coll: MRT (default), BGK, TRT or WMRT; fmt: fast (tensor-factorised) moment
+    transform; hiord: order-12 (untruncated) equilibrium moments; autosym: symmetry
+    node types (reference OPT="d3q19*part*(TRT+BGK+WMRT)*FMT*HiOrd*autosym")."""
     name = "auto"
     m = Model(name, dims=3, family="flow", reference="models/flow/auto",
               description=f"raw-moment {'D3Q19' if q19 else 'D3Q27'} LBM, {coll} collision"
@@ -64,11 +101,17 @@ def build(q19: bool = False, part: bool = False, coll: str = "MRT") -> Model:
     for n in ["EPressure", "EVelocity", "Wall", "WPressure", "WVelocity"]:
         m.add_node_type(n, "BOUNDARY")
     m.add_node_type("MRT", "COLLISION")
-    m.options = {"d3q19": q19, "part": part, "TRT": coll == "TRT", "BGK": coll == "BGK", "WMRT": False}
+    m.options = {"d3q19": q19, "part": part, "TRT": coll == "TRT", "BGK": coll == "BGK", "WMRT": coll == "WMRT",
+                 "FMT": fmt, "HiOrd": hiord, "autosym": autosym}
 
-    raw = mrt_eq(U, orthogonal=False)
-    M = sp.eye(Q) if coll == "BGK" else raw.mat
-    eq = mrt_eq(U, mat=M) if coll == "BGK" else raw
+    raw12 = mrt_eq(U, orthogonal=False, order=12)          # EQ_NO of the reference
+    if coll == "BGK":
+        M = sp.eye(Q)
+    elif coll == "WMRT":
+        M = wmrt_matrix(raw12)
+    else:
+        M = raw12.mat
+    eq = mrt_eq(U, mat=M, order=12 if hiord else 2)
     orders = [int(o) for o in eq.order]
 
     def blocks(_m):
@@ -79,12 +122,27 @@ def build(q19: bool = False, part: bool = False, coll: str = "MRT") -> Model:
             elif coll == "TRT" and o % 2 == 1:
                 om.append("2")            # omega2
             elif coll == "MRT" and o > 2:
-                om.append("1")            # relaxed to equilibrium
+                om.append("1")            # relaxed to equilibrium (WMRT: all at omega)
             else:
                 om.append("0")            # omega
         out = [f"  TCLB_FN static constexpr int om_kind(int k) {{ constexpr int o[{Q}] = {{{', '.join(om)}}}; return o[k]; }}"]
-        out.append(dense_transform("am_moments", eq.mat, Q, Q, "m = f . M"))
-        out.append(dense_transform("am_inverse", eq.mat.inv(), Q, Q, "f = m . M^-1"))
+        if fmt and Q == 27:
+            # FMT: raw moments by three 1-D axis passes, then the (sparse) change of basis
+            # to M (identity for MRT): m = raw . (Mraw^-1 M), f = raw^-1(m . (M^-1 Mraw))
+            pm = poly_matrix(U)
+            T = pm.mat.inv() * eq.mat
+            Ti = eq.mat.inv() * pm.mat
+            out.append(tensor_raw_transform("am_raw", U, pm.p))
+            out.append(tensor_raw_transform("am_rawinv", U, pm.p, inverse=True))
+            out.append(dense_transform("am_r2m", T, Q, Q, "m = raw . Mraw^-1 M"))
+            out.append(dense_transform("am_m2r", Ti, Q, Q, "raw = m . M^-1 Mraw"))
+            out.append("  TCLB_FN static void am_moments(const R* f, R* m) { R r[27]; am_raw(f, r); am_r2m(r, m); }")
+            out.append("  TCLB_FN static void am_inverse(const R* m, R* f) { R r[27]; am_m2r(m, r); am_rawinv(r, f); }")
+        else:
+            # D3Q19 (or no FMT): dense straight-line transforms (the tensor factorisation
+            # needs the full 27-velocity lattice; the moments are the same)
+            out.append(dense_transform("am_moments", eq.mat, Q, Q, "m = f . M"))
+            out.append(dense_transform("am_inverse", eq.mat.inv(), Q, Q, "f = m . M^-1"))
         out.append(exprs_function("am_req", ["rho", "Jx", "Jy", "Jz"], eq.Req))
         out.append(exprs_function("am_feq", ["rho", "Jx", "Jy", "Jz"], eq.feq))
         return "\n".join(out)

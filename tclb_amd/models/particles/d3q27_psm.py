@@ -17,7 +17,10 @@ U27 = [[0, 0, 0], [1, 0, 0], [-1, 0, 0], [0, 1, 0], [0, -1, 0], [0, 0, 1], [0, 0
        [1, 1, -1], [-1, 1, -1], [1, -1, -1], [-1, -1, -1]]
 
 
-def build(ms=False, kl=False, trt=False, nebb=False, sup=False, singlekernel=False) -> Model:
+def build(ms=False, kl=False, trt=False, nebb=False, sup=False, singlekernel=False, sep=False) -> Model:
+    """``sep`` (the ``SEP:singlekernel`` products) is declared only in the reference's
+    conf.mk; neither Dynamics.R nor Dynamics.c.Rt reads Options$SEP, so those variants are
+    the particle-free single-kernel model (Options$particles = NEBB | SUP is false)."""
     m = Model("d3q27_PSM", dims=3, family="particles", reference="models/particles/d3q27_PSM",
               description="D3Q27 partially saturated method for resolved particles")
     particles = nebb or sup
@@ -92,7 +95,7 @@ def build(ms=False, kl=False, trt=False, nebb=False, sup=False, singlekernel=Fal
     m.add_node_type("Solid", "BOUNDARY")
     m.add_node_type("Wall", "BOUNDARY")
     m.add_node_type("BGK", "COLLISION")
-    m.options = {"MS": ms, "KL": kl, "TRT": trt, "NEBB": nebb, "SUP": sup, "singlekernel": singlekernel,
+    m.options = {"SEP": sep, "MS": ms, "KL": kl, "TRT": trt, "NEBB": nebb, "SUP": sup, "singlekernel": singlekernel,
                  "particles": particles}
     m.set_dynamics("particles/d3q27_psm.inc")
     return m

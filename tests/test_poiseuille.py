@@ -17,6 +17,9 @@ CASES = {
     "auto_d3q19_BGK": ((4, 18, 4), {"ForceX": 1e-6}, "Viscosity"),
     "auto_d3q19_TRT": ((4, 18, 4), {"ForceX": 1e-6}, "Viscosity"),
     "auto": ((4, 18, 4), {"ForceX": 1e-6}, "Viscosity"),
+    "auto_WMRT": ((4, 18, 4), {"ForceX": 1e-6}, "Viscosity"),
+    "auto_d3q19_WMRT_HiOrd": ((4, 18, 4), {"ForceX": 1e-6}, "Viscosity"),
+    "auto_FMT_HiOrd": ((4, 18, 4), {"ForceX": 1e-6}, "Viscosity"),
     "d3q27_cumulant_AVG_IB_SMAG": ((4, 18, 4), {"ForceX": 1e-6}, "nu"),
     "d3q27_cumulant_part": ((4, 18, 4), {"ForceX": 1e-6}, "nu"),
     "d3q27_BGK": ((4, 18, 4), {"ForceX": 1e-6}, "nu"),
