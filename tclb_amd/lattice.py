@@ -41,6 +41,9 @@ def eval_expr(expr: str, env: Dict[str, float]) -> float:
     return float(eval(expr, {"__builtins__": {}}, {**_SAFE_MATH, **env}))
 
 
+FIXED_POINT_SWEEPS = 100   # reference: for (int fix=0; fix<100; fix++), src/Lattice.cu.Rt:484
+
+
 def _runs(idx: Sequence[int]) -> List[Tuple[int, int]]:
     """contiguous runs [a, b) of a sorted index list"""
     out = []
@@ -269,7 +272,19 @@ class Lattice:
             fields = self._saved_fields(st)
             if st.particle and self.particles is not None:
                 self.particles.pre_stage(self)
-            if self.overlap and n > 2 * g:
+            if st.fixed_point and k > 0:
+                # fixed-point stage (reference AddStage(fixedPoint=TRUE): 100 sweeps,
+                # src/Lattice.cu.Rt:484).  The reference sweeps in place (input == output
+                # snapshot, an order-dependent Gauss-Seidel on the GPU); here every sweep
+                # reads the current snapshot and writes a scratch one whose saved fields
+                # are copied back: a deterministic Jacobi iteration.
+                scratch = self._scratch_snapshot()
+                for _ in range(FIXED_POINT_SWEEPS):
+                    self._launch_stage(si, dst, scratch, glob)
+                    for r0, r1 in _runs(fields):
+                        dst[r0:r1].copy_(scratch[r0:r1])
+                    self._halo_finish(self._halo_start(dst, fields))
+            elif self.overlap and n > 2 * g:
                 self._launch_stage(si, inp, dst, glob, (0, g))
                 self._launch_stage(si, inp, dst, glob, (n - g, n))
                 hs = self._halo_start(dst, fields)
@@ -285,6 +300,12 @@ class Lattice:
         self.cur = 1 - self.cur
         if glob:
             self._reduce_globals()
+
+    def _scratch_snapshot(self) -> torch.Tensor:
+        if getattr(self, "_scratch", None) is None:
+            self._scratch = torch.zeros(self.nf * self.fs, dtype=self.sdtype, device=self.device).as_strided(
+                self.snaps[0].shape, self.snaps[0].stride())
+        return self._scratch
 
     def _reduce_globals(self):
         g = self.comm.allreduce_globals(self.globals_t, self.model.n_sum_globals)
