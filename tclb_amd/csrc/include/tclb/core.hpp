@@ -191,6 +191,33 @@ TCLB_FN void particle_flush(double* acc, const ParticleS<R>& p) {
 #endif
 }
 
+// Multi-step driver: nsteps of one action (stage list) with A/B snapshot swapping and no
+// host round trip per step (reference Lattice::Iterate, src/Lattice.cu.Rt:900-989).  Used
+// when no halo exchange is needed between stages (one rank, periodic wrap in-kernel);
+// globals are integrated on the last step only when glob_last is set.  L.in holds the
+// current snapshot and L.out the other one on entry.
+template <class Run>
+inline int iterate_action(Launch L, int nsteps, const int* stages, int nstages, int glob_last, Run run) {
+  const void* cur = L.in;
+  void* nxt = L.out;
+  for (int s = 0; s < nsteps; s++) {
+    for (int k = 0; k < nstages; k++) {
+      L.in = k == 0 ? cur : nxt;
+      L.out = nxt;
+      L.stage = stages[k];
+      L.glob = (glob_last && s == nsteps - 1) ? 1 : 0;
+      const int r = run(L);
+      if (r != 0) return r;
+    }
+    L.iter += 1;
+    L.reserved1 += 1;
+    void* t = (void*)cur;
+    cur = nxt;
+    nxt = t;
+  }
+  return 0;
+}
+
 template <class T>
 TCLB_FN T tmax(T a, T b) { return a > b ? a : b; }
 template <class T>

@@ -194,5 +194,17 @@ inline int run_quantity(const Launch& L) {
       default: return -1;                                                                    \
     }                                                                                        \
   }                                                                                          \
+  extern "C" int tclb_##NAME##_iterate(const tclb::Launch* L, int prec, int n, const int* stages,   \
+                                        int nstages, int glob_last) {                          \
+    switch (prec) {                                                                          \
+      case 0: return tclb::iterate_action(*L, n, stages, nstages, glob_last,                 \
+          [](const tclb::Launch& l) { return tclb::exec::run_stage<MODEL, double, double>(l); }); \
+      case 1: return tclb::iterate_action(*L, n, stages, nstages, glob_last,                 \
+          [](const tclb::Launch& l) { return tclb::exec::run_stage<MODEL, float, float>(l); });   \
+      case 2: return tclb::iterate_action(*L, n, stages, nstages, glob_last,                 \
+          [](const tclb::Launch& l) { return tclb::exec::run_stage<MODEL, double, float>(l); });  \
+      default: return -1;                                                                    \
+    }                                                                                        \
+  }                                                                                          \
   extern "C" int tclb_##NAME##_device() { return 1; }                                        \
   extern "C" int tclb_##NAME##_sizeof_launch() { return (int)sizeof(tclb::Launch); }

@@ -58,7 +58,8 @@ def _runs(idx: Sequence[int]) -> List[Tuple[int, int]]:
 class Lattice:
     def __init__(self, model, shape: Tuple[int, int, int], device: Optional[torch.device] = None,
                  precision: str = "double", comm: Optional[Comm] = None, block: Tuple[int, int] = (0, 0),
-                 overlap: Optional[bool] = None, variant: Optional[str] = None):
+                 overlap: Optional[bool] = None, variant: Optional[str] = None, ghosts: Optional[bool] = None,
+                 native_loop: Optional[bool] = None):
         self.model: Model = registry.get(model) if isinstance(model, str) else model.finalize()
         m = self.model
         self.comm = comm or LoopbackComm()
@@ -69,7 +70,10 @@ class Lattice:
         hx, hy, hz = m.halo()
         self.slab: Slab = decompose(gnx, gny, gnz, self.comm.rank, self.comm.size, halo=max(1, hz if gnz > 1 else hy))
         ax = self.slab.axis
-        self.g = max(1, hz if ax == 2 else hy)
+        # ghost planes on the decomposed axis only when ranks exchange halos; a single
+        # rank wraps periodically inside the kernel (Addr::off) and copies nothing
+        self.ghosts = self.comm.distributed if ghosts is None else bool(ghosts)
+        self.g = max(1, hz if ax == 2 else hy) if self.ghosts else 0
         nx, ny, nz = self.slab.local_shape
         self.shape = (nx, ny, nz)
         self.gy = self.g if ax == 1 else 0
@@ -126,6 +130,8 @@ class Lattice:
         self.halo_lo = [i for i, f in enumerate(m.fields) if f.stencil[ax][0] < 0]
         self.halo_hi = [i for i, f in enumerate(m.fields) if f.stencil[ax][1] > 0]
         self._halo_bufs = {}
+        # native multi-step loop (ops.abi ModelLib.iterate) for halo-free lattices
+        self.native_loop = (os.environ.get("TCLB_NATIVE_LOOP", "1") != "0") if native_loop is None else native_loop
         for s in m.settings:
             self.set_setting(s.name, s.default, _init=True)
         self._L = self._base_launch()
@@ -216,6 +222,8 @@ class Lattice:
 
     def _halo_start(self, buf: torch.Tensor, fields: Optional[Sequence[int]] = None):
         g = self.g
+        if g == 0:
+            return None
         n = self.shape[2] if self.slab.axis == 2 else self.shape[1]
         lo = [i for i in self.halo_lo if fields is None or i in fields]
         hi = [i for i in self.halo_hi if fields is None or i in fields]
@@ -318,8 +326,43 @@ class Lattice:
         self.iter = 0
         self.run_action("Init", glob=False)
 
+    def _native_ok(self, action: str) -> bool:
+        if not (self.native_loop and self.lib.has_iterate and self.g == 0 and not self.comm.distributed):
+            return False
+        if self.zseries or self.callbacks or self.particles is not None:
+            return False
+        act = self.model.action(action)
+        return act is not None and not any(self.model.stage(s).fixed_point or self.model.stage(s).particle
+                                           for s in act.stages)
+
     def iterate(self, n: int, glob_last: bool = True, action: str = "Iteration"):
-        """Reference Lattice::Iterate (src/Lattice.cu.Rt:900-989): globals on the last step."""
+        """Reference Lattice::Iterate (src/Lattice.cu.Rt:900-989): globals on the last step.
+
+        Without halos, time series, callbacks or particles the n steps run in one native
+        call (tclb::iterate_action): one kernel launch per stage and no Python per step."""
+        if n <= 0:
+            return
+        if self._native_ok(action):
+            m = self.model
+            stages = [m.stage_index(s) for s in m.action(action).stages]
+            self._sync_settings()
+            if glob_last:
+                self.globals_t.zero_()
+            L = self._L
+            nx, ny, nz = self.shape
+            L.xlo, L.xhi, L.ylo, L.yhi, L.zlo, L.zhi = 0, nx, 0, ny, 0, nz
+            L.in_ = self.snaps[self.cur].data_ptr()
+            L.out = self.snaps[1 - self.cur].data_ptr()
+            L.iter = self.iter
+            L.reserved1 = self.iter - self.average_start + 1
+            L.stream = self._stream()
+            self.lib.iterate(L, self.prec, n, stages, glob_last)
+            self.iter += n
+            if n % 2 == 1:
+                self.cur = 1 - self.cur
+            if glob_last:
+                self._reduce_globals()
+            return
         for i in range(n):
             glob = glob_last and i == n - 1
             if self.zseries:

@@ -272,3 +272,23 @@ family("d2q9q9_cm_cht", ".heat.d2q9q9_cm_cht", "OutFlowConvective*OutFlowNeumann
 family("d3q27q7_cm_cht", ".heat.d3q27q7_cm_cht", "OutFlowConvective*OutFlowNeumann*AVG*IBB*SMAG*CHT")
 family("d3q27q27_cm_cht", ".heat.d3q27q7_cm_cht", "OutFlowConvective*OutFlowNeumann*AVG*IBB*SMAG*CHT", heat_q=27)
 family("d3q27_tePSM_per", ".heat.d3q27_tepsm_per", "(NEBB+SUP)*Isothermal")
+
+
+def register_variant(name: str):
+    """put a family product into the default (pre-built) catalog"""
+    r = _resolve(name)
+    if r is None:
+        raise KeyError(name)
+    register(name, r[0], r[1], **r[2])
+
+
+# products used by reference example cases, and one representative per new option
+for _v in ("d3q27_pf_velocity_thermo", "d3q27_pf_velocity_thermo_planarBenchmark", "d3q27_pf_velocity_OutFlow",
+           "d3q27_pf_velocity_autosym", "d2q9_scmp_Kupershtokh", "d2q9_scmp_LycettLuo",
+           "d2q9_scmp_Kupershtokh_VirtualRhoWBC_ViscositySmooth_CUM", "d2q9_scmp_LycettLuo_WMRT_FMT_HiOrd",
+           "d2q9_csf", "d2q9_csf_noflow", "d2q9_csf_bc_weno_cumulant", "d2q9_csf_bcinit_viscstep",
+           "auto_WMRT", "auto_FMT_HiOrd", "auto_d3q19_TRT_autosym", "wave2D_autosym",
+           "d3q27q27_cm_cht_OutFlowNeumann_AVG_IBB", "d3q27q7_cm_cht_OutFlowNeumann_AVG_IBB",
+           "d2q9q9_cm_cht_OutFlowNeumann_AVG_IBB", "d3q27_cumulant_AVG", "d3q27_cumulant_IB_SMAG",
+           "d3q27_PSM_SEP_singlekernel"):
+    register_variant(_v)

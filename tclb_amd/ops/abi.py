@@ -125,6 +125,22 @@ class ModelLib:
         sz = getattr(self.lib, f"tclb_{model}_sizeof_launch")()
         if sz != ctypes.sizeof(Launch):
             raise KernelError(f"ABI mismatch for {path}: sizeof(Launch) {sz} != {ctypes.sizeof(Launch)}")
+        self._it = getattr(self.lib, f"tclb_{model}_iterate", None)
+        if self._it is not None:
+            self._it.argtypes = [ctypes.POINTER(Launch), ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int),
+                                 ctypes.c_int, ctypes.c_int]
+            self._it.restype = ctypes.c_int
+
+    @property
+    def has_iterate(self) -> bool:
+        return self._it is not None
+
+    def iterate(self, L: Launch, prec: int, n: int, stages, glob_last: bool):
+        """n steps of an action in native code (tclb::iterate_action)"""
+        arr = (ctypes.c_int * len(stages))(*stages)
+        r = self._it(ctypes.byref(L), prec, n, arr, len(stages), 1 if glob_last else 0)
+        if r != 0:
+            raise KernelError(f"{self.model}[{self.kind}] native iterate failed: code {r}")
 
     def run(self, L: Launch, prec: int):
         r = self._run(ctypes.byref(L), prec)

@@ -44,6 +44,15 @@ CASE_SETTINGS = {
                          "CenterX": 20.0, "CenterY": 12.0, "BubbleType": -1.0, "bulk_visc": 0.1666},
     "d2q9_reaction_diffusion_system_SIR_ModifiedPeng": {"Init_N": 1.0, "Init_S": 0.9, "Init_I": 0.1,
                                                         "Beta": 0.3, "Beta_w": 0.2, "Gamma": 0.1},
+    "d2q9_scmp": {"Kupershtokh_K": 0.009, "Temperature": 0.8, "Density": 1.2, "nu_l": 0.1666, "nu_v": 0.1666,
+                  "density_l": 3.0, "density_v": 0.1, "nubuffer": 0.1},
+    "d2q9_csf": {"PhaseField": 0.4, "Mobility": 0.05, "IntWidth": 0.25, "SurfaceTensionRate": 0.01,
+                 "VelocityX": 0.01, "ViscosityStepWidth": 1.0},
+    "d3q27_pf_velocity_thermo": {"Density_h": 1.0, "Density_l": 0.1, "sigma": 1e-3, "Viscosity_l": 0.05,
+                                 "Viscosity_h": 0.05, "M": 0.05, "PhaseField": 1.0, "Radius": 4.0,
+                                 "CenterX": 12.0, "CenterY": 6.0, "CenterZ": 5.0, "BubbleType": -1.0,
+                                 "T_init": 1.0, "dT": 0.05, "sigma_T": -1e-4, "k_h": 0.05, "k_l": 0.02,
+                                 "cp_h": 1.0, "cp_l": 1.0},
     "d3q27_pf_velocity": {"Density_h": 1.0, "Density_l": 0.1, "sigma": 1e-3, "Viscosity_l": 0.05,
                           "Viscosity_h": 0.05, "M": 0.05, "PhaseField": 1.0, "Radius": 4.0,
                           "CenterX": 12.0, "CenterY": 6.0, "CenterZ": 5.0, "BubbleType": -1.0},
@@ -70,7 +79,8 @@ def make_case(name, device="cpu", precision="double", shape=None, comm=None):
         fl[:, :, 0] = wall.value   # x = 0 plane of walls (not on the decomposed axis)
     lat.set_flags(fl)
     for k, v in case_settings(name).items():
-        lat.set_setting(k, v)
+        if m.setting(k) is not None:      # option-dependent settings (e.g. viscstep)
+            lat.set_setting(k, v)
     return lat
 
 

@@ -40,14 +40,11 @@ def test_poiseuille(model):
     nx = shape[0]
     fl = np.full((lat.NZ, lat.NY, nx), coll.value, dtype=np.uint32)
     wall = m.node_type("Wall").value
-    if lat.slab.axis == 2:
-        fl[:, lat.gy + 0, :] = wall
-        fl[:, lat.gy + shape[1] - 1, :] = wall
-    else:
-        fl[:, 0, :] = wall   # ghost row of y=0 plane image is y=ny-1: also wall
-        fl[:, 1, :] = wall
-        fl[:, lat.gy + shape[1] - 1, :] = wall
-        fl[:, -1, :] = wall
+    fl[:, lat.gy + 0, :] = wall
+    fl[:, lat.gy + shape[1] - 1, :] = wall
+    if lat.slab.axis == 1 and lat.gy:     # ghost rows (multi-rank layouts) image the walls
+        fl[:, :lat.gy, :] = wall
+        fl[:, -lat.gy:, :] = wall
     lat.set_flags(fl)
     nu = 1.0 / 6.0
     lat.set_setting(visc, nu)
