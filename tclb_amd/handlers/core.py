@@ -655,49 +655,129 @@ class RunPython(Callback):
 
 @register("Control")
 class Control(GenericAction):
-    """reference conControl (src/Handlers/conControl.cpp:108-257): time-dependent settings.
-    <CSV file= Time=> columns are sampled at every iteration of a control window of
-    ``Iterations`` steps (linear interpolation in time): zonal settings become zonal time
-    series on the lattice (value and slope <name>_DT active at iter % Iterations, the
-    reference's ZoneSettings tables; optimal-control designs act on them), global
-    settings are set every iteration."""
+    """reference conControl (src/Handlers/conControl.cpp:1-257): time-dependent zonal
+    settings over a control window of ``Iterations`` steps.
+
+    ``<CSV file= [Time="expr"]>`` reads a table (unit-aware cells) into a context of
+    columns sampled at every iteration of the window by piecewise-linear interpolation in
+    time; ``Time`` is an expression of the columns (default: rows spread evenly over the
+    window).  ``<Param name= [zone=] value="expr"/>`` (inside a CSV or directly in
+    Control) sets a zonal setting to a time series.  Expressions follow the reference
+    grammar: terms joined by ``+``, each ``Column*scale`` (scale with units), ``Column``
+    or a constant with units after the first term, e.g. ``Sin*0.5m+1m``.
+    Extension: a CSV without Param children applies every column named like a zonal
+    (or ``<setting>-<zone>``) setting directly; global settings named so are set every
+    iteration."""
 
     kind = HANDLER_CALLBACK
+
+    def _expr(self, ctx, expr: str, scale: float) -> np.ndarray:
+        s = self.solver
+        n = len(next(iter(ctx.values()))) if ctx else 1
+        out = np.zeros(n)
+        for i, term in enumerate(expr.split("+")):
+            parts = term.split("*")
+            name = parts[0].strip()
+            if name in ctx:
+                if len(parts) > 2:
+                    raise HandlerError(f"too many '*' in Control expression {expr!r}")
+                k = s.units.alt(parts[1]) if len(parts) == 2 else 1.0
+                out = out + np.asarray(ctx[name]) * k * scale
+            else:
+                if i == 0:
+                    raise HandlerError(f"variable {name} not found in Control context "
+                                       "(syntax: [Variable]*[scale with unit])")
+                if len(parts) > 1:
+                    raise HandlerError(f"too many '*' in Control expression {expr!r}")
+                out = out + s.units.alt(name) * scale
+        return out
+
+    def _param(self, node, ctx):
+        s = self.solver
+        name, zone, value = node.get("name"), node.get("zone"), node.get("value")
+        if value is None:
+            raise HandlerError("Setting value not specified in Param element")
+        if not name:
+            raise HandlerError("Setting name not specified in Param element")
+        st = s.model.setting(name)
+        if st is None or not st.zonal:
+            raise HandlerError(f"Unknown (zonal) setting {name} in Control")
+        if zone and zone not in s.lattice.zone_names:
+            raise HandlerError(f"Unknown zone {zone} (found while setting parameter {name})")
+        vals = self._expr(ctx, value, 1.0) if ctx else np.full(self.length, self._expr({}, value, 1.0)[0])
+        if len(vals) == 1:
+            vals = np.full(self.length, vals[0])
+        s.lattice.set_zone_series(name, vals, zone=zone or None)
+
+    def _csv(self, node):
+        import csv
+        s = self.solver
+        fn = node.get("file")
+        if fn is None:
+            raise HandlerError("No file attribute in CSV in xml config")
+        with open(fn) as f:
+            rows = [r for r in csv.reader(f) if r]
+        if not rows:
+            raise HandlerError(f"Empty file CSV {fn}")
+        names = [h.strip().strip('"') for h in rows[0]]
+        data = {n: [] for n in names}
+        for r in rows[1:]:
+            if len(r) != len(names):
+                raise HandlerError(f"row length does not match the header in CSV file {fn}")
+            for n, v in zip(names, r):
+                data[n].append(s.units.alt(v.strip()))
+        nrow = len(rows) - 1
+        if nrow < 2:
+            raise HandlerError("Not enough records in CSV file")
+        data = {k: np.asarray(v) for k, v in data.items()}
+        data["_index"] = np.arange(nrow, dtype=float)
+        if node.get("Time") is None:
+            t = self._expr(data, "_index", self.length / nrow)
+        else:
+            t = self._expr(data, node.get("Time"), 1.0)
+        it = np.arange(self.length, dtype=float)
+        ctx = {n: np.interp(it, t, data[n]) for n in names}
+        params = [c for c in node if c.tag == "Param"]
+        for c in node:
+            if c.tag != "Param":
+                raise HandlerError(f"Only Param allowed in CSV in Control (found {c.tag})")
+        if params:
+            for c in params:
+                self._param(c, ctx)
+        else:   # extension: columns named like settings
+            for col in names:
+                name, _, zone = col.partition("-")
+                st = s.model.setting(name)
+                if st is None or col == node.get("Time"):
+                    continue
+                if st.zonal:
+                    s.lattice.set_zone_series(name, ctx[col], zone=zone or None)
+                else:
+                    self.series.append((name, ctx[col]))
+        self.context.update(ctx)
 
     def init(self):
         super().init()
         s = self.solver
-        self.series = []  # global settings: (setting, times(array), values(array))
-        length = int(s.units.alt(self.node.get("Iterations", "0")) or 0)
+        self.series = []
+        self.context = {}
+        self.length = int(round(s.units.alt(self.node.get("Iterations", "0")) or 0))
+        if self.length <= 0:
+            raise HandlerError("Zero (or less) iterations in Control element in config")
         for c in self.node:
             if c.tag == "CSV":
-                import csv
-                with open(c.get("file")) as f:
-                    rows = list(csv.DictReader(f))
-                tcol = c.get("Time", "Time")
-                t = np.array([s.units.alt(r[tcol]) for r in rows])
-                n = length or int(round(t.max())) + 1
-                for col in rows[0]:
-                    if col == tcol:
-                        continue
-                    name, _, zone = col.partition("-")
-                    st = s.model.setting(name)
-                    if st is None:
-                        continue
-                    v = np.array([s.units.alt(r[col]) for r in rows])
-                    if st.zonal:
-                        s.lattice.set_zone_series(name, np.interp(np.arange(n), t, v), zone=zone or None)
-                    else:
-                        self.series.append((name, t, v))
+                self._csv(c)
             elif c.tag == "Param":
-                pass
+                self._param(c, self.context)
+            else:
+                raise HandlerError(f"Element {c.tag} not allowed in Control element in config")
         self.every_iter = 1.0 if self.series else 0.0
         return 0
 
     def do_it(self):
         s = self.solver
-        for name, t, v in self.series:
-            s.lattice.set_setting(name, float(np.interp(s.iter, t, v)))
+        for name, v in self.series:
+            s.lattice.set_setting(name, float(v[s.iter % len(v)]))
         return 0
 
 

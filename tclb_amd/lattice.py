@@ -280,7 +280,16 @@ class Lattice:
             fields = self._saved_fields(st)
             if st.particle and self.particles is not None:
                 self.particles.pre_stage(self)
-            if st.fixed_point and k > 0:
+            if st.snapshot_reads and k > 0 and not st.fixed_point:
+                # a stage that reads (through a stencil) a field it also writes: run it
+                # out of place so every node sees the pre-stage values (the reference runs
+                # it in place, an order-dependent race; tools/race_check.py finds these)
+                scratch = self._scratch_snapshot()
+                self._launch_stage(si, dst, scratch, glob)
+                for r0, r1 in _runs(fields):
+                    dst[r0:r1].copy_(scratch[r0:r1])
+                self._halo_finish(self._halo_start(dst, fields))
+            elif st.fixed_point and k > 0:
                 # fixed-point stage (reference AddStage(fixedPoint=TRUE): 100 sweeps,
                 # src/Lattice.cu.Rt:484).  The reference sweeps in place (input == output
                 # snapshot, an order-dependent Gauss-Seidel on the GPU); here every sweep
@@ -332,8 +341,8 @@ class Lattice:
         if self.zseries or self.callbacks or self.particles is not None:
             return False
         act = self.model.action(action)
-        return act is not None and not any(self.model.stage(s).fixed_point or self.model.stage(s).particle
-                                           for s in act.stages)
+        return act is not None and not any(self.model.stage(s).fixed_point or self.model.stage(s).particle or
+                                           self.model.stage(s).snapshot_reads for s in act.stages)
 
     def iterate(self, n: int, glob_last: bool = True, action: str = "Iteration"):
         """Reference Lattice::Iterate (src/Lattice.cu.Rt:900-989): globals on the last step.

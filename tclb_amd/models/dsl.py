@@ -94,6 +94,7 @@ class Stage:
     save_fields: Optional[List[str]] = None   # nicenames; None = all fields
     read_fields: Optional[List[str]] = None   # nicenames read with stencil (for hazard check)
     fixed_point: bool = False
+    snapshot_reads: bool = False   # reads of its own saved fields see the pre-stage values
     particle: bool = False
     init: bool = False                        # "Init" stream: no load before main
 
@@ -257,7 +258,8 @@ class Model:
 
     def add_stage(self, name: str, main: Optional[str] = None, load_densities=False,
                   save_fields=False, read_fields: Optional[Sequence[str]] = None,
-                  fixed_point: bool = False, particle: bool = False, init: bool = False):
+                  fixed_point: bool = False, particle: bool = False, init: bool = False,
+                  snapshot_reads: bool = False):
         """AddStage (src/conf.R:295-330): load_densities / save_fields are True (all), False
         (none) or lists of field names / group tags (reference defaults: FALSE)."""
         if save_fields is True:
@@ -267,7 +269,7 @@ class Model:
         st = Stage(name=name, main=main or name, load_densities=load_densities,
                    save_fields=list(save_fields) if save_fields is not None else None,
                    read_fields=list(read_fields) if read_fields is not None else None,
-                   fixed_point=fixed_point, particle=particle, init=init)
+                   fixed_point=fixed_point, particle=particle, init=init, snapshot_reads=snapshot_reads)
         self.stages = [s for s in self.stages if s.name != name] + [st]
         return st
 

@@ -34,7 +34,10 @@ def build(lycettluo=False, kupershtokh=False, virtualrhowbc=False, viscositysmoo
         m.add_density(f"f[{i}]", int(x), int(y), 0, group="f")
     m.add_field("rho_n", stencil2d=1, group="rho_n")
     m.add_stage("BaseIteration", "Run", save_fields=["f", "nw"], load_densities=["f"])
-    m.add_stage("CalcRhoSC", "CalcRhoSC", save_fields=["rho_n"], load_densities=["f"])
+    # VirtualRhoWBC wall nodes average the neighbours' rho_n while fluid nodes overwrite
+    # rho_n in the same stage: read the pre-stage values (the reference races here)
+    m.add_stage("CalcRhoSC", "CalcRhoSC", save_fields=["rho_n"], load_densities=["f"],
+                snapshot_reads=virtualrhowbc)
     m.add_stage("BaseInit", "Init", save_fields=["f", "rho_n"], load_densities=["f"])
     m.add_action("Init", ["BaseInit"])
     m.add_action("Iteration", ["BaseIteration", "CalcRhoSC"])

@@ -46,7 +46,8 @@ CASE_SETTINGS = {
                                                         "Beta": 0.3, "Beta_w": 0.2, "Gamma": 0.1},
     "d2q9_scmp": {"Kupershtokh_K": 0.009, "Temperature": 0.8, "Density": 1.2, "nu_l": 0.1666, "nu_v": 0.1666,
                   "density_l": 3.0, "density_v": 0.1, "nubuffer": 0.1},
-    "d2q9_csf": {"PhaseField": 0.4, "Mobility": 0.05, "IntWidth": 0.25, "SurfaceTensionRate": 0.01,
+    # no wall plane: the generic perturbation would break the exact -999 wall marker of phi
+    "d2q9_csf": {"_no_walls": True, "PhaseField": -0.45, "Mobility": 0.05, "WettingAngle": 0.5, "IntWidth": 0.25, "SurfaceTensionRate": 0.01,
                  "VelocityX": 0.01, "ViscosityStepWidth": 1.0},
     "d3q27_pf_velocity_thermo": {"Density_h": 1.0, "Density_l": 0.1, "sigma": 1e-3, "Viscosity_l": 0.05,
                                  "Viscosity_h": 0.05, "M": 0.05, "PhaseField": 1.0, "Radius": 4.0,
@@ -75,11 +76,11 @@ def make_case(name, device="cpu", precision="double", shape=None, comm=None):
     nx = shape[0]
     fl = np.full((lat.NZ, lat.NY, nx), collision_value(m), dtype=np.uint32)
     wall = m.node_type("Wall")
-    if wall is not None:
+    if wall is not None and not case_settings(name).get("_no_walls"):
         fl[:, :, 0] = wall.value   # x = 0 plane of walls (not on the decomposed axis)
     lat.set_flags(fl)
     for k, v in case_settings(name).items():
-        if m.setting(k) is not None:      # option-dependent settings (e.g. viscstep)
+        if not k.startswith("_") and m.setting(k) is not None:      # option-dependent settings (e.g. viscstep)
             lat.set_setting(k, v)
     return lat
 

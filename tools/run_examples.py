@@ -70,6 +70,8 @@ def main():
     ap.add_argument("--device", default="cpu")
     ap.add_argument("--out", default="/tmp/tclb_examples")
     ap.add_argument("--timeout", type=int, default=1200)
+    ap.add_argument("--cwd", default=None, help="working directory (default: the case's directory; the "
+                                                 "reference resolves data paths like example/... from its root)")
     a = ap.parse_args()
     ok = 0
     for case in a.cases:
@@ -85,7 +87,7 @@ def main():
         t0 = time.time()
         try:
             r = subprocess.run([sys.executable, "-m", "tclb_amd", model, tmp, "--device", a.device],
-                               cwd=os.path.dirname(os.path.abspath(case)), capture_output=True, text=True,
+                               cwd=a.cwd or os.path.dirname(os.path.abspath(case)), capture_output=True, text=True,
                                timeout=a.timeout, env={**os.environ, "PYTHONPATH": REPO})
             rec["status"] = "ok" if r.returncode == 0 else f"rc={r.returncode}"
             rec["tail"] = (r.stdout + r.stderr)[-600:]
