@@ -540,25 +540,93 @@ class _Optimizer(GenericAction):
 
 @register("Optimize")
 class Optimize(_Optimizer):
-    """maximise the Objective over the design parameters (reference acOptimize: NLopt,
-    Method MMA/LBFGS/..., MaxEvaluations, tolerances)"""
+    """maximise the Objective over the design parameters (reference acOptimize,
+    src/Handlers/acOptimize.cpp.Rt:1-140, NLopt).  ``method``: MMA (default; the
+    conservative moving-asymptotes method of tclb_amd.utils.mma), LBFGS (L-BFGS-B),
+    COBYLA, NELDERMEAD (derivative-free, scipy), DIRECT_L (scipy ``direct``, locally
+    biased) and ESCH (evolutionary; scipy differential evolution stands in for NLopt's
+    ESCH).  Stopping criteria: MaxEvaluations, RelTolerance, AbsTolerance,
+    XAbsTolerance, StopAtValue.  ``Material="more|less"`` adds the inequality
+    constraint sum(x) >= / <= sum(x0) (tolerance 1e-3)."""
+
+    METHODS = ("LBFGS", "MMA", "COBYLA", "NELDERMEAD", "DIRECT_L", "ESCH")
 
     def init(self):
         super().init()
-        from scipy.optimize import minimize
+        import scipy.optimize as so
+        from ..utils.mma import mma_minimize
+        n = self.node
         x0, lo, hi = self._prepare()
-        method = (self.node.get("Method", "MMA") or "MMA").upper()
-        sp_method = "SLSQP" if method in ("SLSQP", "COBYLA") else "L-BFGS-B"
-        maxev = int(float(self.node.get("MaxEvaluations", "20")))
-        tol = self.node.get("RelTolerance")
-        res = minimize(lambda x: tuple(-v for v in self._evaluate(x)), x0, jac=True, method=sp_method,
-                       bounds=list(zip(lo, hi)),
-                       options={"maxiter": maxev, **({"maxfun": maxev} if sp_method == "L-BFGS-B" else {})},
-                       tol=float(tol) if tol else None)
+        x0 = np.clip(x0, lo, hi)
+        method = (n.get("method") or n.get("Method") or "MMA").upper()
+        if method not in self.METHODS:
+            raise HandlerError(f"Unknown Method in Optimize: {method}")
+
+        def pos(attr, conv=float):
+            v = n.get(attr)
+            if v is None:
+                return None
+            v = conv(float(v))
+            if v <= 0:
+                raise HandlerError(f"{attr} in Optimize have to be above 0")
+            return v
+        maxev = pos("MaxEvaluations", int) or 1000
+        ftol_rel, ftol_abs, xtol = pos("RelTolerance"), pos("AbsTolerance"), pos("XAbsTolerance")
+        stopval = float(n.get("StopAtValue")) if n.get("StopAtValue") is not None else None
+        material = float(np.sum(x0))
+        mat = n.get("Material")
+        if mat not in (None, "more", "less"):
+            raise HandlerError('Material attribute in Optimize should be "more" or "less"')
+        sign = {"more": 1.0, "less": -1.0}.get(mat)
+        cache = {}
+
+        def f_neg(x):                               # NLopt maximises; minimise -J
+            key = x.tobytes()
+            if key not in cache:
+                J, g = self._evaluate(np.asarray(x, dtype=float))
+                cache.clear()
+                cache[key] = (-J, -g)
+            return cache[key]
+        if method == "MMA":
+            cons = []
+            if sign is not None:   # more: material - sum(x) <= 0 ; less: sum(x) - material <= 0
+                cons.append(lambda x: (sign * (material - np.sum(x)) - 1e-3, -sign * np.ones_like(x)))
+            r = mma_minimize(f_neg, x0, lo, hi, constraints=cons, maxeval=maxev, ftol_rel=ftol_rel or 0.0,
+                             ftol_abs=ftol_abs or 0.0, xtol_abs=xtol or 0.0,
+                             stopval=None if stopval is None else -stopval)
+            xbest, fbest, msg = r.x, r.f, r.message
+        else:
+            cons = ()
+            if sign is not None:
+                cons = ({"type": "ineq", "fun": lambda x: sign * (np.sum(x) - material) + 1e-3,
+                         "jac": lambda x: sign * np.ones_like(x)},)
+            bounds = list(zip(lo, hi))
+            fun = lambda x: f_neg(x)[0]   # noqa: E731
+            if method == "LBFGS":
+                res = so.minimize(f_neg, x0, jac=True, method="L-BFGS-B" if not cons else "SLSQP", bounds=bounds,
+                                  constraints=cons, tol=ftol_rel,
+                                  options={"maxiter": maxev, **({} if cons else {"maxfun": maxev})})
+            elif method == "COBYLA":
+                bc = [{"type": "ineq", "fun": (lambda x, i=i: x[i] - lo[i])} for i in range(x0.size)] + \
+                     [{"type": "ineq", "fun": (lambda x, i=i: hi[i] - x[i])} for i in range(x0.size)]
+                res = so.minimize(fun, x0, method="COBYLA", constraints=list(cons) + bc,
+                                  options={"maxiter": maxev, **({"tol": xtol} if xtol else {})})
+            elif method == "NELDERMEAD":
+                res = so.minimize(fun, x0, method="Nelder-Mead", bounds=bounds,
+                                  options={"maxfev": maxev, **({"xatol": xtol} if xtol else {}),
+                                           **({"fatol": ftol_abs} if ftol_abs else {})})
+            elif method == "DIRECT_L":
+                res = so.direct(fun, bounds, maxfun=maxev, locally_biased=True)
+            else:  # ESCH
+                res = so.differential_evolution(fun, bounds, maxiter=max(1, maxev // (15 * x0.size)), polish=False,
+                                                seed=0, constraints=() if not cons else
+                                                so.LinearConstraint(sign * np.ones((1, x0.size)),
+                                                                    sign * material - 1e-3, np.inf))
+            xbest, fbest, msg = np.asarray(res.x), float(res.fun), str(getattr(res, "message", ""))
         self.solver.lattice.snaps[self.solver.lattice.cur].copy_(self.state0)
-        _set_all(self.solver, res.x)
-        self.solver.optimum = (-res.fun, res.x)
-        log.notice(f"Optimize finished after {self.evals} evaluations: objective {-res.fun:.10g} ({res.message})")
+        _set_all(self.solver, xbest)
+        self.solver.optimum = (-fbest, xbest)
+        log.notice(f"Optimize [{method}] finished after {self.evals} evaluations: objective {-fbest:.10g} ({msg})")
         return 0
 
 

@@ -114,3 +114,18 @@ def test_extrude_topology_gradient(tmp_path):
     for i, adj, fd in s.fdtest:
         assert abs(adj - fd) <= 1e-5 * abs(fd) + 1e-12, (i, adj, fd)
         assert abs(fd) > 0
+
+
+@pytest.mark.parametrize("method", ["MMA", "LBFGS", "COBYLA", "NELDERMEAD"])
+def test_optimize_methods_and_material_constraint(tmp_path, method):
+    """reference attribute ``method`` (NLopt names) and Material="less": the design's total
+    material may not grow (tolerance 1e-3, as NLopt's inequality constraint)"""
+    s = run(tmp_path, "<InternalTopology/>",
+            f'<Optimize MaxEvaluations="6" method="{method}" Material="less">'
+            '<Adjoint type="unsteady"><Solve Iterations="6"/></Adjoint></Optimize>')
+    best, x = s.optimum
+    assert np.isfinite(best) and len(s.opt_history) >= 1
+    x0_sum = 36 * 1.0          # InternalTopology starts fully fluid (w = 1)
+    assert x.sum() <= x0_sum + 1e-3 + 1e-9
+    if method in ("MMA", "LBFGS"):
+        assert best >= s.opt_history[0] - 1e-12
