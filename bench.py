@@ -11,7 +11,9 @@ MRT collision everywhere, body force ForceX; uniform initial state (synthetic ca
 as BASELINE.json prescribes).  Each timed step is the full reference iteration
 (collide-stream of every node + boundary + halo exchange; globals on the last step
 of the window, as Lattice::Iterate does).  Compute and storage precision: fp64
-(the reference default, src/configure.ac:208-211) unless --precision float.
+(the reference default, src/configure.ac:208-211) unless --precision names one of the
+reduced-storage modes (mixed[-shift]: fp64 compute / fp32 storage, half[-shift]: fp32
+compute / fp16 storage; *-shift stores f - w_i, reference --with-storage=...-shift).
 """
 from __future__ import annotations
 
@@ -27,6 +29,7 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 from tclb_amd.lattice import Lattice  # noqa: E402
+from tclb_amd.ops.abi import PRECISIONS  # noqa: E402
 from tclb_amd.parallel.comm import init_distributed_from_env  # noqa: E402
 
 METRIC = "MLUPS (million lattice updates/sec) whole-node, d3q27 512^3, at 1/2/4/8 MI355X"
@@ -51,7 +54,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--size", type=int, default=512)
     ap.add_argument("--model", default="d3q27")
-    ap.add_argument("--precision", default="double", choices=["double", "float", "mixed"])
+    ap.add_argument("--precision", default="double", choices=list(PRECISIONS))
     ap.add_argument("--weak", action="store_true", help="size^3 per GPU (z-extent x N)")
     ap.add_argument("--block", default="0,0")
     ap.add_argument("--no-overlap", action="store_true")
@@ -98,7 +101,7 @@ def main():
     mlups = nodes * a.steps / dt / 1e6
     ok = bool(np.isfinite(lat.globals.get("XFlux", 0.0)))
     if rank == 0:
-        es = 8 if a.precision == "double" else 4
+        es = lat.snaps[0].element_size()
         nf = lat.nf
         bytes_node = 2 * nf * es + (2 if lat.model.flag_bits == 16 else 4)
         out = {
@@ -112,7 +115,10 @@ def main():
             "higher_is_better": True,
             "scaling": "weak" if a.weak else "strong",
             "vs_baseline": None,
-            "dtype": {"double": "fp64", "float": "fp32", "mixed": "fp64-compute/fp32-storage"}[a.precision],
+            "dtype": {"double": "fp64", "float": "fp32", "float-shift": "fp32 (shifted storage)",
+                      "mixed": "fp64-compute/fp32-storage", "mixed-shift": "fp64-compute/fp32-shifted-storage",
+                      "half": "fp32-compute/fp16-storage",
+                      "half-shift": "fp32-compute/fp16-shifted-storage"}[a.precision],
             "data": "synthetic (uniform init, channel walls + body force, random-free)",
             "config": {"model": a.model, "global_batch": nodes, "seq_len": shape[0],
                        "lattice": list(shape), "parallelism": f"zslab{world}" if world > 1 else "single",

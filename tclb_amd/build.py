@@ -91,6 +91,76 @@ def _cmd(kind: str, src: str, out: str, gen_dir: str, variant: str = "") -> List
             "-Wno-unused-variable", *incs, src, "-o", out]
 
 
+_PY_STAMP: Optional[str] = None
+_PKG = os.path.dirname(os.path.abspath(__file__))
+
+
+def _rel_hash(paths: Iterable[str], extra: str = "") -> str:
+    """like _hash_inputs but independent of where the tree lives (the snapshot a GPU box
+    runs sits at another path than the tree the libraries were built in)"""
+    h = hashlib.sha1(extra.replace(_PKG, "<pkg>").encode())
+    for p in sorted(paths, key=lambda q: os.path.relpath(q, _PKG)):
+        with open(p, "rb") as f:
+            h.update(os.path.relpath(p, _PKG).encode())
+            h.update(f.read())
+    return h.hexdigest()
+
+
+def _python_stamp() -> str:
+    """hash of the model definitions and the emitter (everything a generated header
+    depends on besides csrc): any edit there may change a model's code"""
+    global _PY_STAMP
+    if _PY_STAMP is None:
+        files = []
+        for sub in ("models", "emit"):
+            for d, _, fs in os.walk(os.path.join(_PKG, sub)):
+                files += [os.path.join(d, f) for f in fs if f.endswith(".py")]
+        _PY_STAMP = _rel_hash(files)
+    return _PY_STAMP
+
+
+def source_stamp(name: str, kind: str, variant: str = "") -> str:
+    """cheap fingerprint of everything a model library is built from (the Python model
+    definition and emitter, the csrc headers and dynamics includes, the compile command),
+    stored next to the library as <lib>.src and checked by ops.abi.load without emitting"""
+    model = registry.get(name)
+    gdir = os.path.join(BUILD, "gen", name)
+    v = variant if kind == "hip" else ""
+    cmd = _cmd(kind, os.path.join(gdir, "kernels_" + kind), lib_path(name, kind, v), gdir, v)
+    return _rel_hash(_deps_no_gen(model.dynamics), " ".join(cmd) + _python_stamp())
+
+
+def _deps_no_gen(dynamics: Optional[str]) -> List[str]:
+    inc = os.path.join(CSRC, "include", "tclb")
+    deps = [os.path.join(inc, f) for f in os.listdir(inc) if f.endswith((".hpp", ".h"))]
+    todo, seen = ([dynamics] if dynamics else []), set()
+    while todo:
+        rel = todo.pop()
+        p = os.path.join(CSRC, "models", rel)
+        if rel in seen or not os.path.exists(p):
+            continue
+        seen.add(rel)
+        deps.append(p)
+        with open(p) as f:
+            todo += [ln.strip().split('"')[1] for ln in f if ln.strip().startswith("#include \"")]
+    return deps
+
+
+def stale_reason(name: str, kind: str, variant: str = "") -> Optional[str]:
+    """None when the library exists and was built from the current sources"""
+    v = variant if kind == "hip" else ""
+    target = lib_path(name, kind, v)
+    if not os.path.exists(target):
+        return "missing"
+    stamp = target + ".src"
+    if not os.path.exists(stamp):
+        return "no source stamp"
+    with open(stamp) as f:
+        if f.read() != source_stamp(name, kind, variant):
+            return "sources changed since it was built"
+    return None
+
+
 def build_model(name: str, kinds=("cpu", "hip"), force: bool = False, verbose: bool = False,
                 variant: str = "") -> Dict[str, str]:
     model = registry.get(name)
@@ -107,6 +177,7 @@ def build_model(name: str, kinds=("cpu", "hip"), force: bool = False, verbose: b
         h = _hash_inputs(_deps(paths["dir"], model.dynamics), " ".join(cmd))
         stamp = target + ".hash"
         if not force and os.path.exists(target) and os.path.exists(stamp) and open(stamp).read() == h:
+            _write_src_stamp(name, kind, variant)
             out[kind] = target
             continue
         t0 = time.time()
@@ -118,10 +189,20 @@ def build_model(name: str, kinds=("cpu", "hip"), force: bool = False, verbose: b
         os.replace(tmp, target)
         with open(stamp, "w") as f:
             f.write(h)
+        _write_src_stamp(name, kind, variant)
         if verbose:
             print(f"[tclb build] {name} [{kind}{'/' + v if v else ''}] {time.time() - t0:.1f}s", flush=True)
         out[kind] = target
     return out
+
+
+def _write_src_stamp(name: str, kind: str, variant: str):
+    v = variant if kind == "hip" else ""
+    s = source_stamp(name, kind, variant)
+    p = lib_path(name, kind, v) + ".src"
+    if not os.path.exists(p) or open(p).read() != s:
+        with open(p, "w") as f:
+            f.write(s)
 
 
 def build_host(force: bool = False, verbose: bool = False) -> str:

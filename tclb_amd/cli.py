@@ -12,6 +12,7 @@ import os
 import sys
 import xml.etree.ElementTree as ET
 
+from .ops.abi import PRECISIONS
 from .utils.log import log
 
 
@@ -21,7 +22,7 @@ def main(argv=None):
     ap.add_argument("config", nargs="?", help="XML case file")
     ap.add_argument("edits", nargs="*", help="XPath edits: 'XPATH = value', 'XPATH @attr = value', ...")
     ap.add_argument("--device", default=None, choices=[None, "cpu", "cuda"])
-    ap.add_argument("--precision", default="double", choices=["double", "float", "mixed"])
+    ap.add_argument("--precision", default="double", choices=list(PRECISIONS))
     ap.add_argument("--list", action="store_true")
     ap.add_argument("--describe", action="store_true")
     a = ap.parse_intermixed_args(argv)   # options may follow the model / case file

@@ -66,7 +66,64 @@ struct Launch {
   const void* ext[6];
   long long next[6];       // element counts of the ext slots
   double time_shift;       // synthetic-turbulence time wave number (Lattice.set_turbulence)
+  int storage_shift;       // 1: reduced-precision storage keeps f - shift(field) (see below)
+  int reserved2;
 };
+
+// Reduced-precision storage (reference --with-storage=float|half[-shift],
+// src/configure.ac:213-233, src/LatticeAccess.inc.cpp.Rt:14-35).  A density is stored as
+// f_i - w_i (w_i: the rest equilibrium of its lattice, Model::field_shift) when
+// Launch.storage_shift is set, so fp32/fp16 keep the relative precision of the small
+// deviation from rest instead of that of f_i ~ w_i.  Applied only when the storage type
+// is narrower than double.  half_t: IEEE binary16 (native _Float16 in hipcc; a bit-exact
+// round-to-nearest-even software conversion for the g++ CPU executor).
+#if TCLB_GPU
+typedef _Float16 half_t;
+#else
+struct half_t {
+  uint16_t b;
+  half_t() = default;
+  half_t(double d) : b(from_float((float)d)) {}
+  operator double() const { return (double)to_float(b); }
+  static uint16_t from_float(float f) {
+    uint32_t x;
+    __builtin_memcpy(&x, &f, 4);
+    const uint32_t sign = (x >> 16) & 0x8000u;
+    const uint32_t ax = x & 0x7fffffffu;
+    if (ax >= 0x7f800000u) return (uint16_t)(sign | 0x7c00u | (ax > 0x7f800000u ? 0x200u : 0u));
+    if (ax >= 0x477ff000u) return (uint16_t)(sign | 0x7c00u);   // rounds to >= 65520: inf
+    if (ax < 0x38800000u) {                                     // subnormal half (or zero)
+      if (ax < 0x33000000u) return (uint16_t)sign;
+      const uint32_t e = ax >> 23, m = (ax & 0x7fffffu) | 0x800000u;
+      const uint32_t s = 126u - e;                               // 14..24
+      uint32_t h = m >> s;
+      const uint32_t rem = m & ((1u << s) - 1u), half = 1u << (s - 1u);
+      if (rem > half || (rem == half && (h & 1u))) h++;
+      return (uint16_t)(sign | h);
+    }
+    uint32_t h = ((ax - 0x38000000u) >> 13);
+    const uint32_t rem = ax & 0x1fffu;
+    if (rem > 0x1000u || (rem == 0x1000u && (h & 1u))) h++;
+    return (uint16_t)(sign | h);
+  }
+  static float to_float(uint16_t h) {
+    const uint32_t sign = (uint32_t)(h & 0x8000u) << 16;
+    uint32_t e = (h >> 10) & 0x1fu, m = h & 0x3ffu, x;
+    if (e == 0) {
+      if (m == 0) x = sign;
+      else {
+        e = 113;
+        while (!(m & 0x400u)) { m <<= 1; e--; }
+        x = sign | (e << 23) | ((m & 0x3ffu) << 13);
+      }
+    } else if (e == 31) x = sign | 0x7f800000u | (m << 13);
+    else x = sign | ((e + 112u) << 23) | (m << 13);
+    float f;
+    __builtin_memcpy(&f, &x, 4);
+    return f;
+  }
+};
+#endif
 
 // Periodic wrap helper for non-decomposed axes.
 TCLB_FN int wrap(int v, int n) { return v < 0 ? v + n : (v >= n ? v - n : v); }
@@ -191,13 +248,43 @@ TCLB_FN void particle_flush(double* acc, const ParticleS<R>& p) {
 #endif
 }
 
+// Probe plan of the Sampler (reference src/Sampler.cpp:66-80, Lattice::updateAllSamples
+// src/Lattice.cu.Rt:1376-1389): after every step the nq quantities are evaluated at np
+// points (local coordinates) into out[row][np][width] (double, unit-scaled), so a whole
+// callback interval is recorded on the device and copied to the host once.  One launch
+// per step covers every point and quantity (the reference launches one per point and
+// quantity).
+constexpr int SAMPLE_MAXQ = 32;
+struct SamplePlan {
+  const int* points;   // device int[np][3]
+  double* out;         // device double[rows][np][width]
+  int np, width;       // points, values per point (sum of ncomp)
+  int row, rows;       // row written after the first step of a call / capacity
+  int nq;
+  int q[SAMPLE_MAXQ], ncomp[SAMPLE_MAXQ], offset[SAMPLE_MAXQ];
+  double scale[SAMPLE_MAXQ];
+};
+
+// one probe of node n into o[width] (shared by both executors)
+template <class NodeT>
+TCLB_FN void sample_node(NodeT& n, const SamplePlan& P, double* o) {
+  n.pop();
+  for (int i = 0; i < P.nq; i++) {
+    typename NodeT::real_t v[3] = {0, 0, 0};
+    n.get_quantity(P.q[i], v);
+    for (int c = 0; c < P.ncomp[i]; c++) o[P.offset[i] + c] = (double)v[c] * P.scale[i];
+  }
+}
+
 // Multi-step driver: nsteps of one action (stage list) with A/B snapshot swapping and no
 // host round trip per step (reference Lattice::Iterate, src/Lattice.cu.Rt:900-989).  Used
 // when no halo exchange is needed between stages (one rank, periodic wrap in-kernel);
 // globals are integrated on the last step only when glob_last is set.  L.in holds the
-// current snapshot and L.out the other one on entry.
-template <class Run>
-inline int iterate_action(Launch L, int nsteps, const int* stages, int nstages, int glob_last, Run run) {
+// current snapshot and L.out the other one on entry.  With a sample plan the probes of
+// every step are recorded (row sp->row + s) after the step.
+template <class Run, class Sample>
+inline int iterate_action(Launch L, int nsteps, const int* stages, int nstages, int glob_last,
+                          const SamplePlan* sp, Run run, Sample sample) {
   const void* cur = L.in;
   void* nxt = L.out;
   for (int s = 0; s < nsteps; s++) {
@@ -214,9 +301,78 @@ inline int iterate_action(Launch L, int nsteps, const int* stages, int nstages, 
     void* t = (void*)cur;
     cur = nxt;
     nxt = t;
+    if (sp != nullptr && sp->np > 0 && sp->row + s < sp->rows) {
+      Launch Q = L;
+      Q.in = cur;
+      Q.out = nxt;
+      Q.glob = 0;
+      Q.reserved1 = L.reserved1 > 2 ? L.reserved1 - 1 : 1;   // quantity averaging count
+      SamplePlan P = *sp;
+      P.row = sp->row + s;
+      const int r = sample(Q, P);
+      if (r != 0) return r;
+    }
   }
   return 0;
 }
+
+// Precision codes of the C ABI (mirrored by ops/abi.py PREC):
+//   0 fp64 compute / fp64 storage (reference default, src/configure.ac:208-211)
+//   1 fp32 compute / fp32 storage
+//   2 fp64 compute / fp32 storage (reference --with-storage=float[-shift])
+//   3 fp32 compute / fp16 storage (reference --with-storage=half[-shift])
+// the *-shift variants are the same instantiations with Launch.storage_shift = 1.
+template <class R_, class S_>
+struct prec_tag {
+  typedef R_ R;
+  typedef S_ S;
+};
+template <class F>
+inline int prec_dispatch(int prec, F&& f) {
+  switch (prec) {
+    case 0: return f(prec_tag<double, double>{});
+    case 1: return f(prec_tag<float, float>{});
+    case 2: return f(prec_tag<double, float>{});
+    case 3: return f(prec_tag<float, half_t>{});
+    default: return -1;
+  }
+}
+
+// C exports common to both executors (each defines tclb::exec::run_stage, run_quantity
+// and run_sample for its device).
+#define TCLB_EXPORT_COMMON(NAME, MODEL)                                                       \
+  extern "C" int tclb_##NAME##_run(const tclb::Launch* L, int prec) {                         \
+    return tclb::prec_dispatch(prec, [&](auto t) {                                            \
+      using T = decltype(t);                                                                  \
+      return tclb::exec::run_stage<MODEL, typename T::R, typename T::S>(*L);                  \
+    });                                                                                       \
+  }                                                                                           \
+  extern "C" int tclb_##NAME##_quantity(const tclb::Launch* L, int prec) {                    \
+    return tclb::prec_dispatch(prec, [&](auto t) {                                            \
+      using T = decltype(t);                                                                  \
+      return tclb::exec::run_quantity<MODEL, typename T::R, typename T::S>(*L);               \
+    });                                                                                       \
+  }                                                                                           \
+  extern "C" int tclb_##NAME##_iterate(const tclb::Launch* L, int prec, int n, const int* stages, \
+                                        int nstages, int glob_last, const tclb::SamplePlan* sp) { \
+    return tclb::prec_dispatch(prec, [&](auto t) {                                            \
+      using T = decltype(t);                                                                  \
+      return tclb::iterate_action(                                                            \
+          *L, n, stages, nstages, glob_last, sp,                                              \
+          [](const tclb::Launch& l) { return tclb::exec::run_stage<MODEL, typename T::R, typename T::S>(l); }, \
+          [](const tclb::Launch& l, const tclb::SamplePlan& p) {                              \
+            return tclb::exec::run_sample<MODEL, typename T::R, typename T::S>(l, p);         \
+          });                                                                                 \
+    });                                                                                       \
+  }                                                                                           \
+  extern "C" int tclb_##NAME##_sample(const tclb::Launch* L, int prec, const tclb::SamplePlan* P) { \
+    return tclb::prec_dispatch(prec, [&](auto t) {                                            \
+      using T = decltype(t);                                                                  \
+      return tclb::exec::run_sample<MODEL, typename T::R, typename T::S>(*L, *P);             \
+    });                                                                                       \
+  }                                                                                           \
+  extern "C" int tclb_##NAME##_sizeof_sample_plan() { return (int)sizeof(tclb::SamplePlan); } \
+  extern "C" int tclb_##NAME##_sizeof_launch() { return (int)sizeof(tclb::Launch); }
 
 template <class T>
 TCLB_FN T tmax(T a, T b) { return a > b ? a : b; }

@@ -75,37 +75,21 @@ inline int run_quantity(const Launch& L) {
   return 0;
 }
 
+template <class Model, class R, class S>
+inline int run_sample(const Launch& L, const SamplePlan& P) {
+  if (P.np <= 0 || P.row < 0 || P.row >= P.rows) return 0;
+  for (int p = 0; p < P.np; p++) {
+    const int* c = P.points + 3 * p;
+    R g[1];
+    typename Model::template NodeT<R, S, false> n(L, c[0], c[1], c[2], g);
+    sample_node(n, P, P.out + ((long long)P.row * P.np + p) * P.width);
+  }
+  return 0;
+}
+
 }  // namespace exec
 }  // namespace tclb
 
 #define TCLB_EXPORT_MODEL(NAME, MODEL)                                                       \
-  extern "C" int tclb_##NAME##_run(const tclb::Launch* L, int prec) {                        \
-    switch (prec) {                                                                          \
-      case 0: return tclb::exec::run_stage<MODEL, double, double>(*L);                       \
-      case 1: return tclb::exec::run_stage<MODEL, float, float>(*L);                         \
-      case 2: return tclb::exec::run_stage<MODEL, double, float>(*L);                        \
-      default: return -1;                                                                    \
-    }                                                                                        \
-  }                                                                                          \
-  extern "C" int tclb_##NAME##_quantity(const tclb::Launch* L, int prec) {                   \
-    switch (prec) {                                                                          \
-      case 0: return tclb::exec::run_quantity<MODEL, double, double>(*L);                    \
-      case 1: return tclb::exec::run_quantity<MODEL, float, float>(*L);                      \
-      case 2: return tclb::exec::run_quantity<MODEL, double, float>(*L);                     \
-      default: return -1;                                                                    \
-    }                                                                                        \
-  }                                                                                          \
-  extern "C" int tclb_##NAME##_iterate(const tclb::Launch* L, int prec, int n, const int* stages,   \
-                                        int nstages, int glob_last) {                          \
-    switch (prec) {                                                                          \
-      case 0: return tclb::iterate_action(*L, n, stages, nstages, glob_last,                 \
-          [](const tclb::Launch& l) { return tclb::exec::run_stage<MODEL, double, double>(l); }); \
-      case 1: return tclb::iterate_action(*L, n, stages, nstages, glob_last,                 \
-          [](const tclb::Launch& l) { return tclb::exec::run_stage<MODEL, float, float>(l); });   \
-      case 2: return tclb::iterate_action(*L, n, stages, nstages, glob_last,                 \
-          [](const tclb::Launch& l) { return tclb::exec::run_stage<MODEL, double, float>(l); });  \
-      default: return -1;                                                                    \
-    }                                                                                        \
-  }                                                                                          \
-  extern "C" int tclb_##NAME##_device() { return 0; }                                        \
-  extern "C" int tclb_##NAME##_sizeof_launch() { return (int)sizeof(tclb::Launch); }
+  TCLB_EXPORT_COMMON(NAME, MODEL)                                                            \
+  extern "C" int tclb_##NAME##_device() { return 0; }

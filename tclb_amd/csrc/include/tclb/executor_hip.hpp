@@ -120,6 +120,17 @@ __global__ void __launch_bounds__(256) k_quantity(const Launch L) {
   for (int c = 0; c < nc; c++) out[idx + (long long)c * L.qcomp] = o[c] * R(L.qscale);
 }
 
+// Sampler probes: one thread per point, every quantity of the plan (core.hpp SamplePlan).
+template <class Model, class R, class S>
+__global__ void __launch_bounds__(64) k_sample(const Launch L, const SamplePlan P) {
+  const int p = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+  if (p >= P.np) return;
+  const int* c = P.points + 3 * p;
+  R g[1];
+  typename Model::template NodeT<R, S, false> n(L, c[0], c[1], c[2], g);
+  sample_node(n, P, P.out + ((long long)P.row * P.np + p) * P.width);
+}
+
 // Default shapes from on-device A/B (profiles/r01_tune_*): fp64 storage 128x2, fp32 256x1.
 inline void launch_shape(const Launch& L, dim3& grid, dim3& block, int sbytes = 8) {
   const int w = L.xhi - L.xlo, h = L.yhi - L.ylo, d = L.zhi - L.zlo;
@@ -171,40 +182,17 @@ inline int run_quantity(const Launch& L) {
   return (int)hipGetLastError();
 }
 
+template <class Model, class R, class S>
+inline int run_sample(const Launch& L, const SamplePlan& P) {
+  if (P.np <= 0 || P.row < 0 || P.row >= P.rows) return 0;
+  k_sample<Model, R, S><<<dim3((P.np + 63) / 64), dim3(64), 0, (hipStream_t)L.stream>>>(L, P);
+  return (int)hipGetLastError();
+}
+
 }  // namespace exec
 }  // namespace tclb
 
-// C ABI: prec 0 = fp64 compute / fp64 storage (reference default, src/configure.ac:208-211)
-//        prec 1 = fp32 compute / fp32 storage
-//        prec 2 = fp64 compute / fp32 storage (reference --with-storage=float)
+// C ABI (precision codes: core.hpp prec_dispatch)
 #define TCLB_EXPORT_MODEL(NAME, MODEL)                                                       \
-  extern "C" int tclb_##NAME##_run(const tclb::Launch* L, int prec) {                        \
-    switch (prec) {                                                                          \
-      case 0: return tclb::exec::run_stage<MODEL, double, double>(*L);                       \
-      case 1: return tclb::exec::run_stage<MODEL, float, float>(*L);                         \
-      case 2: return tclb::exec::run_stage<MODEL, double, float>(*L);                        \
-      default: return -1;                                                                    \
-    }                                                                                        \
-  }                                                                                          \
-  extern "C" int tclb_##NAME##_quantity(const tclb::Launch* L, int prec) {                   \
-    switch (prec) {                                                                          \
-      case 0: return tclb::exec::run_quantity<MODEL, double, double>(*L);                    \
-      case 1: return tclb::exec::run_quantity<MODEL, float, float>(*L);                      \
-      case 2: return tclb::exec::run_quantity<MODEL, double, float>(*L);                     \
-      default: return -1;                                                                    \
-    }                                                                                        \
-  }                                                                                          \
-  extern "C" int tclb_##NAME##_iterate(const tclb::Launch* L, int prec, int n, const int* stages,   \
-                                        int nstages, int glob_last) {                          \
-    switch (prec) {                                                                          \
-      case 0: return tclb::iterate_action(*L, n, stages, nstages, glob_last,                 \
-          [](const tclb::Launch& l) { return tclb::exec::run_stage<MODEL, double, double>(l); }); \
-      case 1: return tclb::iterate_action(*L, n, stages, nstages, glob_last,                 \
-          [](const tclb::Launch& l) { return tclb::exec::run_stage<MODEL, float, float>(l); });   \
-      case 2: return tclb::iterate_action(*L, n, stages, nstages, glob_last,                 \
-          [](const tclb::Launch& l) { return tclb::exec::run_stage<MODEL, double, float>(l); });  \
-      default: return -1;                                                                    \
-    }                                                                                        \
-  }                                                                                          \
-  extern "C" int tclb_##NAME##_device() { return 1; }                                        \
-  extern "C" int tclb_##NAME##_sizeof_launch() { return (int)sizeof(tclb::Launch); }
+  TCLB_EXPORT_COMMON(NAME, MODEL)                                                            \
+  extern "C" int tclb_##NAME##_device() { return 1; }

@@ -80,7 +80,7 @@ class Geometry:
     k along that axis are ``(lo - g + k) mod n_global``."""
 
     def __init__(self, model, gshape: Tuple[int, int, int], slab_lo: int, slab_n: int, axis: int, ghost: int,
-                 units: Optional[UnitEnv] = None, permissive: bool = False):
+                 units: Optional[UnitEnv] = None, permissive: bool = False, yz: Optional[Tuple[int, ...]] = None):
         self.model = model
         self.gnx, self.gny, self.gnz = gshape
         self.axis = axis
@@ -88,7 +88,11 @@ class Geometry:
         self.permissive = permissive
         self.total = Region(0, 0, 0, self.gnx, self.gny, self.gnz)
         g = ghost
-        if axis == 2:
+        if axis == 3:               # Y x Z grid block: yz = (ylo, ny, gy, zlo, nz, gz)
+            ylo, ny, gy, zlo, nz, gz = yz
+            ys = (np.arange(ny + 2 * gy) + ylo - gy) % self.gny
+            zs = (np.arange(nz + 2 * gz) + zlo - gz) % self.gnz
+        elif axis == 2:
             zs = (np.arange(slab_n + 2 * g) + slab_lo - g) % self.gnz
             ys = np.arange(self.gny)
         else:

@@ -108,8 +108,9 @@ class GeometryAction(Action):
         from ..geometry.geometry import Geometry
         s = self.solver
         lat = s.lattice
-        g = Geometry(s.model, lat.gshape, lat.slab.lo, lat.slab.n, lat.slab.axis, lat.g, units=s.units,
-                     permissive=s.permissive)
+        sl = lat.slab
+        g = Geometry(s.model, lat.gshape, sl.lo, sl.n, sl.axis, lat.g, units=s.units, permissive=s.permissive,
+                     yz=(sl.ylo, sl.ny, lat.gy, sl.zlo, sl.nz, lat.gz) if sl.axis == 3 else None)
         g.load(self.node)
         s.geometry = g
         lat.set_flags(g.flags)
@@ -518,48 +519,60 @@ class DumpSettings(Callback):
 @register("Sample")
 class Sample(Callback):
     """reference cbSample + Sampler (src/Handlers/cbSample.cpp:5-60, src/Sampler.cpp:16-99):
-    probe points, quantities appended to a CSV on the owning rank"""
+    the quantities at the probe points are recorded EVERY iteration on the device
+    (tclb_amd.sampler, reference Lattice::updateAllSamples) and written at each callback:
+    one CSV row per iteration and point, columns Iteration,X,Y,Z,<quantities> (vectors
+    as .x/.y/.z), SI units.  Rows of all ranks are gathered to rank 0, which writes the
+    file (the reference lets every owning rank append to it).  The Iteration column is the
+    iteration count after the sampled step."""
 
     def init(self):
         super().init()
+        from ..sampler import Sampler as _Probes
         s = self.solver
+        if not self.every_iter:
+            raise HandlerError("Iteration value in sampler should not be zero")
         self.what = _what(self.node)
-        self.points = []
-        for p in self.node.findall("Point"):
+        points = []
+        for p in self.node:
+            if p.tag != "Point":
+                raise HandlerError(f"Unknown element in Sampler: {p.tag}")
             x = int(round(s.units.alt(p.get("dx", "0"))))
             y = int(round(s.units.alt(p.get("dy", "0"))))
             z = int(round(s.units.alt(p.get("dz", "0"))))
-            self.points.append((x, y, z))
-        self.fn = s.out_iter_file(self.node.get("name", "Sampler"), ".csv")
-        self.qs = [q for q in s.model.quantities if "all" in self.what or q.name in self.what]
-        lat = s.lattice
-        ox, oy, oz = lat.slab.offset
-        nx, ny, nz = lat.shape
-        self.mine = [(i, p) for i, p in enumerate(self.points)
-                     if oy <= p[1] < oy + ny and oz <= p[2] < oz + nz and 0 <= p[0] < nx]
-        if self.mine:
+            if all(0 <= v < n for v, n in zip((x, y, z), s.lattice.gshape)):
+                points.append((x, y, z))
+        self.fn = s.out_iter_file("Sampler", ".csv")
+        qs = [q for q in s.model.quantities if ("all" in self.what or q.name in self.what) and not q.adjoint]
+        scales = {q.name: 1.0 / s.units.unit_scale(q.unit) for q in qs}
+        self.probes = _Probes(s.lattice, points, [q.name for q in qs], scales, rows=int(math.ceil(self.every_iter)))
+        s.lattice.samplers.append(self.probes)
+        if s.rank == 0:
             with open(self.fn, "w") as f:
-                cols = ["Iteration", "point", "x", "y", "z"]
-                for q in self.qs:
-                    cols += [q.name + c for c in (".x", ".y", ".z")] if q.vector else [q.name]
-                f.write(",".join(cols) + "\n")
+                f.write(",".join(["Iteration", "X", "Y", "Z"] + self.probes.columns) + "\n")
         return 0
 
-    def do_it(self):
-        if not self.mine:
-            return 0
+    def _write(self):
         s = self.solver
-        lat = s.lattice
-        ox, oy, oz = lat.slab.offset
-        vals = {q.name: s.quantity_si(q.name) for q in self.qs}
+        rows = self.probes.flush()
+        if s.comm.distributed:
+            rows = [r for part in s.comm.gather_objects(rows) or [] for r in part]
+        if s.rank != 0:
+            return
+        rows.sort(key=lambda r: (r[0], r[1]))
         with open(self.fn, "a") as f:
-            for i, (x, y, z) in self.mine:
-                row = [str(s.iter), str(i), str(x), str(y), str(z)]
-                for q in self.qs:
-                    a = vals[q.name][:, z - oz, y - oy, x]
-                    row += [f"{v:.13e}" for v in a]
-                f.write(",".join(row) + "\n")
+            for it, _, (x, y, z), v in rows:
+                f.write(",".join([str(it), str(x), str(y), str(z)] + [f"{a:.13e}" for a in v]) + "\n")
+
+    def do_it(self):
+        self._write()
         return 0
+
+    def finish(self):
+        if self.probes in self.solver.lattice.samplers:
+            self._write()
+            self.solver.lattice.samplers.remove(self.probes)
+        return super().finish()
 
 
 @register("PID")

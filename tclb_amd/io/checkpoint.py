@@ -17,15 +17,19 @@ import torch
 MAGIC = "tclb_amd-checkpoint-1"
 
 
-def _np_dtype(t):
-    return np.float32 if t == torch.float32 else np.float64
+def _np_dtype(lat):
+    """storage dtype, except that shifted (f - w) and fp16 storage are written as fp64
+    true values so the file stays portable across precisions"""
+    if lat.storage_shift or lat.sdtype == torch.float16:
+        return np.float64
+    return np.float32 if lat.sdtype == torch.float32 else np.float64
 
 
 def save_state(solver, prefix: str) -> str:
     lat = solver.lattice
     path = prefix if prefix.endswith(".tclb") else prefix + ".tclb"
     gnx, gny, gnz = lat.gshape
-    dt = _np_dtype(lat.sdtype)
+    dt = _np_dtype(lat)
     shape = (lat.nf, gnz, gny, gnx)
     if solver.rank == 0:
         os.makedirs(os.path.dirname(path) or ".", exist_ok=True)
@@ -63,7 +67,7 @@ def load_state(solver, path: str, comp=None):
     ox, oy, oz = lat.slab.offset
     nx, ny, nz = lat.shape
     data = np.array(mm[:, oz:oz + nz, oy:oy + ny, :])
-    t = torch.from_numpy(data).to(lat.device, dtype=lat.sdtype)
+    t = torch.from_numpy(data).to(lat.device, dtype=torch.float64)
     if comp is not None:
         cur = lat.fields_interior().clone()
         idx = [i for i, f in enumerate(lat.model.fields) if f.group == comp or f.nicename == comp or f.name == comp]

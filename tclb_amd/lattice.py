@@ -29,6 +29,7 @@ from .models.dsl import Model
 from .ops import abi
 from .parallel.comm import Comm, LoopbackComm
 from .parallel.decomp import Slab, decompose
+from .utils import trace
 
 _SAFE_MATH = {k: getattr(math, k) for k in ("sqrt", "exp", "log", "sin", "cos", "tan", "atan", "atan2", "pi",
                                               "pow", "fabs", "floor", "ceil", "tanh", "sinh", "cosh", "acos", "asin")}
@@ -59,7 +60,7 @@ class Lattice:
     def __init__(self, model, shape: Tuple[int, int, int], device: Optional[torch.device] = None,
                  precision: str = "double", comm: Optional[Comm] = None, block: Tuple[int, int] = (0, 0),
                  overlap: Optional[bool] = None, variant: Optional[str] = None, ghosts: Optional[bool] = None,
-                 native_loop: Optional[bool] = None):
+                 native_loop: Optional[bool] = None, grid: Optional[Tuple[int, int]] = None):
         self.model: Model = registry.get(model) if isinstance(model, str) else model.finalize()
         m = self.model
         self.comm = comm or LoopbackComm()
@@ -68,16 +69,24 @@ class Lattice:
             raise ValueError(f"2-D model {m.name} needs nz=1")
         self.gshape = (gnx, gny, gnz)
         hx, hy, hz = m.halo()
-        self.slab: Slab = decompose(gnx, gny, gnz, self.comm.rank, self.comm.size, halo=max(1, hz if gnz > 1 else hy))
+        # 1-D slab, or a Y x Z grid (grid=(py, pz), env TCLB_GRID="py,pz", or automatic
+        # when the slab axis is too thin for the rank count; parallel/decomp.py)
+        if grid is None and os.environ.get("TCLB_GRID"):
+            grid = tuple(int(v) for v in os.environ["TCLB_GRID"].split(","))
+        self.slab: Slab = decompose(gnx, gny, gnz, self.comm.rank, self.comm.size, halo=max(1, hz if gnz > 1 else hy),
+                                    grid=grid, halo_y=max(1, hy))
         ax = self.slab.axis
         # ghost planes on the decomposed axis only when ranks exchange halos; a single
         # rank wraps periodically inside the kernel (Addr::off) and copies nothing
-        self.ghosts = self.comm.distributed if ghosts is None else bool(ghosts)
+        self.ghosts = (self.comm.distributed or ax == 3) if ghosts is None else bool(ghosts)
         self.g = max(1, hz if ax == 2 else hy) if self.ghosts else 0
         nx, ny, nz = self.slab.local_shape
         self.shape = (nx, ny, nz)
         self.gy = self.g if ax == 1 else 0
         self.gz = self.g if ax == 2 else 0
+        if ax == 3:                       # ghosts on both split axes
+            self.gy, self.gz = max(1, hy), max(1, hz)
+            self.g = max(self.gy, self.gz)
         if ax == 2 and hy > ny:
             raise ValueError("y stencil larger than domain")
         self.px = ((nx + 63) // 64) * 64 if nx >= 64 else ((nx + 7) // 8) * 8
@@ -85,10 +94,17 @@ class Lattice:
         self.NZ = nz + 2 * self.gz
         self.device = torch.device(device) if device is not None else torch.device("cpu")
         self.is_gpu = self.device.type == "cuda"
+        if precision not in abi.PRECISIONS:
+            raise ValueError(f"unknown precision {precision!r}: one of {', '.join(abi.PRECISIONS)}")
         self.precision = precision
-        self.prec = abi.PREC[precision]
-        self.sdtype = torch.float32 if precision in ("float", "mixed") else torch.float64
-        self.rdtype = torch.float32 if precision == "float" else torch.float64
+        self.prec, self.storage_shift = abi.PRECISIONS[precision]
+        self.sdtype = {0: torch.float64, 1: torch.float32, 2: torch.float32, 3: torch.float16}[self.prec]
+        self.rdtype = torch.float64 if self.prec in (0, 2) else torch.float32
+        # per-field storage shift (f - w_i) of the *-shift modes, as a (nf,1,1,1) tensor
+        self._shift_t = None
+        if self.storage_shift:
+            from .emit.emitter import field_shifts
+            self._shift_t = torch.tensor(field_shifts(m), dtype=torch.float64, device=self.device).view(-1, 1, 1, 1)
         nf = len(m.fields)
         self.nf = nf
         plane = self.NZ * self.NY * self.px
@@ -123,12 +139,15 @@ class Lattice:
         self.globals: Dict[str, float] = {g.name: 0.0 for g in m.globals_}
         self.iter = 0
         self.block = block
-        self.overlap = self.comm.distributed if overlap is None else overlap
+        self.overlap = (self.comm.distributed if overlap is None else overlap) and ax != 3
         kind = "hip" if self.is_gpu else "cpu"
         self.lib = abi.load(m.name, kind, variant=variant)
-        # halo field sets: fields read from below (stencil min < 0) / above (max > 0) along axis
-        self.halo_lo = [i for i, f in enumerate(m.fields) if f.stencil[ax][0] < 0]
-        self.halo_hi = [i for i, f in enumerate(m.fields) if f.stencil[ax][1] > 0]
+        # halo field sets per split axis: fields read from below (stencil min < 0) /
+        # above (max > 0) along that axis
+        self.halo_sets = {a: ([i for i, f in enumerate(m.fields) if f.stencil[a][0] < 0],
+                              [i for i, f in enumerate(m.fields) if f.stencil[a][1] > 0])
+                          for a in ((1, 2) if ax == 3 else (ax,))}
+        self.halo_lo, self.halo_hi = self.halo_sets[2 if ax == 3 else ax]
         self._halo_bufs = {}
         # native multi-step loop (ops.abi ModelLib.iterate) for halo-free lattices
         self.native_loop = (os.environ.get("TCLB_NATIVE_LOOP", "1") != "0") if native_loop is None else native_loop
@@ -136,6 +155,7 @@ class Lattice:
             self.set_setting(s.name, s.default, _init=True)
         self._L = self._base_launch()
         self.callbacks = []
+        self.samplers = []        # tclb_amd.sampler.Sampler: probes recorded every iteration
         self.turb_t = None
         self.turb_time_wn = 0.0
         self.cuts = None
@@ -157,6 +177,7 @@ class Lattice:
         L.xlo, L.xhi, L.ylo, L.yhi, L.zlo, L.zhi = 0, nx, 0, ny, 0, nz
         L.block_x, L.block_y = self.block
         L.flags = self.flags.data_ptr()
+        L.storage_shift = 1 if self.storage_shift else 0
         return L
 
     def _sync_settings(self):
@@ -200,58 +221,78 @@ class Lattice:
             else:
                 L.ylo, L.yhi = axis_range
         self.lib.run(L, self.prec)
+        if trace.SYNC:
+            trace.after_launch(self, f"{self.model.name} stage {stage}")
 
     # ------------------------------------------------------------------ halos
-    def _axis_planes(self, buf: torch.Tensor, a: int, b: int) -> torch.Tensor:
-        """view of planes [a, b) in ghost-inclusive coordinates along the decomposed axis"""
-        return buf[:, a:b] if self.slab.axis == 2 else buf[:, :, a:b]
+    def _axis_planes(self, buf: torch.Tensor, a: int, b: int, axis: Optional[int] = None) -> torch.Tensor:
+        """view of planes [a, b) in ghost-inclusive coordinates along a split axis
+        (default: the slab axis; 1 = y rows, 2 = z planes)"""
+        axis = self.slab.axis if axis is None else axis
+        return buf[:, a:b] if axis == 2 else buf[:, :, a:b]
 
-    def _pack(self, buf: torch.Tensor, fields: List[int], a: int, b: int) -> torch.Tensor:
-        planes = self._axis_planes(buf, a, b)
+    def _pack(self, buf: torch.Tensor, fields: List[int], a: int, b: int, axis: Optional[int] = None) -> torch.Tensor:
+        planes = self._axis_planes(buf, a, b, axis)
         runs = _runs(fields)
         if len(runs) == 1:
             return planes[runs[0][0]:runs[0][1]].contiguous()
         return torch.cat([planes[r0:r1] for r0, r1 in runs], 0).contiguous()
 
-    def _unpack(self, buf: torch.Tensor, fields: List[int], a: int, b: int, data: torch.Tensor):
-        planes = self._axis_planes(buf, a, b)
+    def _unpack(self, buf: torch.Tensor, fields: List[int], a: int, b: int, data: torch.Tensor,
+                axis: Optional[int] = None):
+        planes = self._axis_planes(buf, a, b, axis)
         k = 0
         for r0, r1 in _runs(fields):
             planes[r0:r1].copy_(data[k:k + (r1 - r0)])
             k += r1 - r0
 
     def _halo_start(self, buf: torch.Tensor, fields: Optional[Sequence[int]] = None):
-        g = self.g
-        if g == 0:
+        if self.g == 0:
             return None
-        n = self.shape[2] if self.slab.axis == 2 else self.shape[1]
-        lo = [i for i in self.halo_lo if fields is None or i in fields]
-        hi = [i for i in self.halo_hi if fields is None or i in fields]
+        if self.slab.axis == 3:
+            # Y x Z grid: z planes first, then y rows over the whole z extent (ghosts
+            # included), which also fills the edge ghosts; no overlap split
+            for a in (2, 1):
+                self._halo_finish(self._halo_axis_start(buf, fields, a))
+            return None
+        return self._halo_axis_start(buf, fields, self.slab.axis)
+
+    def _halo_axis_start(self, buf: torch.Tensor, fields: Optional[Sequence[int]], axis: int):
+        g = self.gz if axis == 2 else self.gy
+        n = self.shape[2] if axis == 2 else self.shape[1]
+        lo_set, hi_set = self.halo_sets[axis]
+        lo = [i for i in lo_set if fields is None or i in fields]
+        hi = [i for i in hi_set if fields is None or i in fields]
         if not self.comm.distributed:
             # loopback: periodic wrap = plane copies inside this snapshot
             for r0, r1 in _runs(lo):
-                self._axis_planes(buf, 0, g)[r0:r1].copy_(self._axis_planes(buf, n, n + g)[r0:r1])
+                self._axis_planes(buf, 0, g, axis)[r0:r1].copy_(self._axis_planes(buf, n, n + g, axis)[r0:r1])
             for r0, r1 in _runs(hi):
-                self._axis_planes(buf, n + g, n + 2 * g)[r0:r1].copy_(self._axis_planes(buf, g, 2 * g)[r0:r1])
+                self._axis_planes(buf, n + g, n + 2 * g, axis)[r0:r1].copy_(self._axis_planes(buf, g, 2 * g, axis)[r0:r1])
             return None
-        send_up = self._pack(buf, lo, n, n + g) if lo else None        # my top planes -> next's lower ghost
-        send_down = self._pack(buf, hi, g, 2 * g) if hi else None      # my bottom planes -> prev's upper ghost
+        if trace.ENABLED:
+            trace.push("halo")
+        send_up = self._pack(buf, lo, n, n + g, axis) if lo else None        # my top planes -> next's lower ghost
+        send_down = self._pack(buf, hi, g, 2 * g, axis) if hi else None      # my bottom planes -> prev's upper ghost
         recv_below = torch.empty_like(send_up) if lo else None
         recv_above = torch.empty_like(send_down) if hi else None
-        h = self.comm.start_halo(send_up, send_down, recv_below, recv_above)
-        return (h, buf, lo, hi, recv_below, recv_above, send_up, send_down)
+        nbr = self.slab.neighbours(axis) if self.slab.axis == 3 else None
+        h = self.comm.start_halo(send_up, send_down, recv_below, recv_above, nbr=nbr)
+        return (h, buf, lo, hi, recv_below, recv_above, send_up, send_down, axis)
 
     def _halo_finish(self, st):
         if st is None:
             return
-        h, buf, lo, hi, rb, ra, su, sd = st
+        h, buf, lo, hi, rb, ra, su, sd, axis = st
         self.comm.wait_halo(h)
-        g = self.g
-        n = self.shape[2] if self.slab.axis == 2 else self.shape[1]
+        g = self.gz if axis == 2 else self.gy
+        n = self.shape[2] if axis == 2 else self.shape[1]
         if lo:
-            self._unpack(buf, lo, 0, g, rb)
+            self._unpack(buf, lo, 0, g, rb, axis)
         if hi:
-            self._unpack(buf, hi, n + g, n + 2 * g, ra)
+            self._unpack(buf, hi, n + g, n + 2 * g, ra, axis)
+        if trace.ENABLED:
+            trace.pop()
 
     def exchange(self, buf: Optional[torch.Tensor] = None, fields=None):
         buf = self.snaps[self.cur] if buf is None else buf
@@ -273,7 +314,11 @@ class Lattice:
             self.globals_t.zero_()
         n = self.shape[2] if self.slab.axis == 2 else self.shape[1]
         g = self.g
+        if trace.ENABLED:
+            trace.push(f"action {name}")
         for k, sname in enumerate(act.stages):
+            if trace.ENABLED:
+                trace.push(f"stage {sname}")
             si = m.stage_index(sname)
             st = m.stage(sname)
             inp = src if k == 0 else dst
@@ -314,9 +359,13 @@ class Lattice:
                 self.particles.post_stage(self)
                 if name != "Init":
                     self.particles.step(self)
+            if trace.ENABLED:
+                trace.pop()
         self.cur = 1 - self.cur
         if glob:
             self._reduce_globals()
+        if trace.ENABLED:
+            trace.pop()
 
     def _scratch_snapshot(self) -> torch.Tensor:
         if getattr(self, "_scratch", None) is None:
@@ -325,7 +374,8 @@ class Lattice:
         return self._scratch
 
     def _reduce_globals(self):
-        g = self.comm.allreduce_globals(self.globals_t, self.model.n_sum_globals)
+        with trace.span("globals"):
+            g = self.comm.allreduce_globals(self.globals_t, self.model.n_sum_globals)
         vals = g.detach().cpu().numpy()
         for i, gl in enumerate(self.model.globals_):
             self.globals[gl.name] = float(vals[i])
@@ -338,7 +388,7 @@ class Lattice:
     def _native_ok(self, action: str) -> bool:
         if not (self.native_loop and self.lib.has_iterate and self.g == 0 and not self.comm.distributed):
             return False
-        if self.zseries or self.callbacks or self.particles is not None:
+        if self.zseries or self.callbacks or self.particles is not None or len(self.samplers) > 1:
             return False
         act = self.model.action(action)
         return act is not None and not any(self.model.stage(s).fixed_point or self.model.stage(s).particle or
@@ -365,7 +415,13 @@ class Lattice:
             L.iter = self.iter
             L.reserved1 = self.iter - self.average_start + 1
             L.stream = self._stream()
-            self.lib.iterate(L, self.prec, n, stages, glob_last)
+            smp = self.samplers[0] if self.samplers else None
+            with trace.span(f"iterate {action} x{n}"):
+                self.lib.iterate(L, self.prec, n, stages, glob_last, smp.plan_for(n) if smp else None)
+            if trace.SYNC:
+                trace.after_launch(self, f"{self.model.name} native loop")
+            if smp:
+                smp.advance(n)
             self.iter += n
             if n % 2 == 1:
                 self.cur = 1 - self.cur
@@ -378,6 +434,8 @@ class Lattice:
                 self.apply_series()
             self.run_action(action, glob=glob)
             self.iter += 1
+            for smp in self.samplers:
+                smp.sample_now()
             for cb in self.callbacks:
                 cb(self)
 
@@ -516,14 +574,24 @@ class Lattice:
         """interior view of a stored field in the current snapshot: (nz, ny, nx)"""
         i = self.model.field_index(name)
         nx, ny, nz = self.shape
-        return self.snaps[self.cur][i, self.gz:self.gz + nz, self.gy:self.gy + ny, :nx]
+        v = self.snaps[self.cur][i, self.gz:self.gz + nz, self.gy:self.gy + ny, :nx]
+        if self._shift_t is not None:        # shifted storage: a copy of the true values
+            return v.to(self.rdtype) + self._shift_t[i, 0].to(self.rdtype)
+        return v
 
     def fields_interior(self) -> torch.Tensor:
+        """all fields on the interior (nf, nz, ny, nx): a view of the storage, or for the
+        *-shift precisions a copy with the storage shift added back"""
         nx, ny, nz = self.shape
-        return self.snaps[self.cur][:, self.gz:self.gz + nz, self.gy:self.gy + ny, :nx]
+        v = self.snaps[self.cur][:, self.gz:self.gz + nz, self.gy:self.gy + ny, :nx]
+        if self._shift_t is not None:
+            return v.to(self.rdtype) + self._shift_t.to(self.rdtype)
+        return v
 
     def set_fields_interior(self, data: torch.Tensor):
         nx, ny, nz = self.shape
+        if self._shift_t is not None:
+            data = data.to(torch.float64) - self._shift_t
         self.snaps[self.cur][:, self.gz:self.gz + nz, self.gy:self.gy + ny, :nx].copy_(data)
         self.exchange()
 
@@ -606,5 +674,5 @@ class Lattice:
         return self.gshape[0] * self.gshape[1] * self.gshape[2]
 
     def memory_bytes(self) -> int:
-        es = 4 if self.sdtype == torch.float32 else 8
+        es = self.snaps[0].element_size()
         return 2 * self.nf * self.fs * es + self.flags.numel() * self.flags.element_size()

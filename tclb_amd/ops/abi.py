@@ -10,6 +10,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import sys
 import threading
 from typing import Dict, Optional
 
@@ -50,10 +51,40 @@ class Launch(ctypes.Structure):
         ("ext", ctypes.c_void_p * 6),
         ("next", ctypes.c_longlong * 6),
         ("time_shift", ctypes.c_double),
+        ("storage_shift", ctypes.c_int),
+        ("reserved2", ctypes.c_int),
     ]
 
 
-PREC = {"double": 0, "float": 1, "mixed": 2}
+# precision name -> (C ABI code of the compute/storage instantiation, shifted storage);
+# reference --with-storage=double|float|float-shift|half|half-shift (src/configure.ac:213-233)
+PRECISIONS = {
+    "double": (0, False),          # fp64 compute, fp64 storage
+    "float": (1, False),           # fp32 compute, fp32 storage
+    "float-shift": (1, True),      # fp32 compute, fp32 storage of f - w
+    "mixed": (2, False),           # fp64 compute, fp32 storage
+    "mixed-shift": (2, True),      # fp64 compute, fp32 storage of f - w
+    "half": (3, False),            # fp32 compute, fp16 storage
+    "half-shift": (3, True),       # fp32 compute, fp16 storage of f - w
+}
+PREC = {k: v[0] for k, v in PRECISIONS.items()}
+
+SAMPLE_MAXQ = 32
+
+
+class SamplePlan(ctypes.Structure):
+    """mirror of tclb::SamplePlan (csrc/include/tclb/core.hpp)"""
+    _fields_ = [
+        ("points", ctypes.c_void_p),
+        ("out", ctypes.c_void_p),
+        ("np", ctypes.c_int), ("width", ctypes.c_int),
+        ("row", ctypes.c_int), ("rows", ctypes.c_int),
+        ("nq", ctypes.c_int),
+        ("q", ctypes.c_int * SAMPLE_MAXQ),
+        ("ncomp", ctypes.c_int * SAMPLE_MAXQ),
+        ("offset", ctypes.c_int * SAMPLE_MAXQ),
+        ("scale", ctypes.c_double * SAMPLE_MAXQ),
+    ]
 
 
 class AdCtx(ctypes.Structure):
@@ -125,22 +156,34 @@ class ModelLib:
         sz = getattr(self.lib, f"tclb_{model}_sizeof_launch")()
         if sz != ctypes.sizeof(Launch):
             raise KernelError(f"ABI mismatch for {path}: sizeof(Launch) {sz} != {ctypes.sizeof(Launch)}")
-        self._it = getattr(self.lib, f"tclb_{model}_iterate", None)
-        if self._it is not None:
-            self._it.argtypes = [ctypes.POINTER(Launch), ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int),
-                                 ctypes.c_int, ctypes.c_int]
-            self._it.restype = ctypes.c_int
+        sp = getattr(self.lib, f"tclb_{model}_sizeof_sample_plan")()
+        if sp != ctypes.sizeof(SamplePlan):
+            raise KernelError(f"ABI mismatch for {path}: sizeof(SamplePlan) {sp} != {ctypes.sizeof(SamplePlan)}")
+        self._it = getattr(self.lib, f"tclb_{model}_iterate")
+        self._it.argtypes = [ctypes.POINTER(Launch), ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int),
+                             ctypes.c_int, ctypes.c_int, ctypes.POINTER(SamplePlan)]
+        self._it.restype = ctypes.c_int
+        self._smp = getattr(self.lib, f"tclb_{model}_sample")
+        self._smp.argtypes = [ctypes.POINTER(Launch), ctypes.c_int, ctypes.POINTER(SamplePlan)]
+        self._smp.restype = ctypes.c_int
 
     @property
     def has_iterate(self) -> bool:
-        return self._it is not None
+        return True
 
-    def iterate(self, L: Launch, prec: int, n: int, stages, glob_last: bool):
-        """n steps of an action in native code (tclb::iterate_action)"""
+    def iterate(self, L: Launch, prec: int, n: int, stages, glob_last: bool, plan: Optional[SamplePlan] = None):
+        """n steps of an action in native code (tclb::iterate_action), recording the
+        sampler probes of every step when a plan is given"""
         arr = (ctypes.c_int * len(stages))(*stages)
-        r = self._it(ctypes.byref(L), prec, n, arr, len(stages), 1 if glob_last else 0)
+        r = self._it(ctypes.byref(L), prec, n, arr, len(stages), 1 if glob_last else 0,
+                     ctypes.byref(plan) if plan is not None else None)
         if r != 0:
             raise KernelError(f"{self.model}[{self.kind}] native iterate failed: code {r}")
+
+    def sample(self, L: Launch, prec: int, plan: SamplePlan):
+        r = self._smp(ctypes.byref(L), prec, ctypes.byref(plan))
+        if r != 0:
+            raise KernelError(f"{self.model}[{self.kind}] sample failed: code {r}")
 
     def run(self, L: Launch, prec: int):
         r = self._run(ctypes.byref(L), prec)
@@ -166,7 +209,15 @@ def load(model: str, kind: str, build_if_missing: bool = True, variant: Optional
         if key in _libs:
             return _libs[key]
         path = B.lib_path(model, kind, variant)
-        if build_if_missing and (not os.path.exists(path) or os.environ.get("TCLB_REBUILD")):
+        # a library built from other sources than the current ones is never loaded
+        # silently: rebuild it (hash-stamped, usually seconds) or fail
+        stale = "forced" if os.environ.get("TCLB_REBUILD") else B.stale_reason(model, kind, variant)
+        if stale is not None:
+            if not build_if_missing or os.environ.get("TCLB_NO_BUILD"):
+                raise KernelError(f"kernel library for model '{model}' [{kind}] is not usable ({stale}): {path}; "
+                                  f"run python -m tclb_amd.build {model}")
+            if stale != "missing":
+                print(f"[tclb] rebuilding {os.path.basename(path)}: {stale}", file=sys.stderr, flush=True)
             B.build_model(model, kinds=(kind,), variant=variant)
         if not os.path.exists(path):
             raise KernelError(f"kernel library for model '{model}' [{kind}] not built: {path}")

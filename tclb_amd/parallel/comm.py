@@ -42,7 +42,9 @@ class Comm:
         return [obj]
 
     def start_halo(self, send_up: Optional[torch.Tensor], send_down: Optional[torch.Tensor],
-                   recv_below: Optional[torch.Tensor], recv_above: Optional[torch.Tensor]):
+                   recv_below: Optional[torch.Tensor], recv_above: Optional[torch.Tensor], nbr=None):
+        """send_up -> next, send_down -> prev, recv_below <- prev, recv_above <- next;
+        nbr = (prev, next) ranks (default: rank -+ 1, the slab neighbours)"""
         raise NotImplementedError
 
     def wait_halo(self, handle):
@@ -59,7 +61,7 @@ class LoopbackComm(Comm):
     def __init__(self, exercise_dist_path: bool = False):
         self.distributed = exercise_dist_path
 
-    def start_halo(self, send_up, send_down, recv_below, recv_above):
+    def start_halo(self, send_up, send_down, recv_below, recv_above, nbr=None):
         if send_up is not None:
             recv_below.copy_(send_up)
         if send_down is not None:
@@ -118,19 +120,20 @@ class TorchDistComm(Comm):
         self.dist.all_gather_object(out, obj, group=self.group)
         return out
 
-    def start_halo(self, send_up, send_down, recv_below, recv_above):
+    def start_halo(self, send_up, send_down, recv_below, recv_above, nbr=None):
         d = self.dist
+        prev, nxt = nbr if nbr is not None else (self.prev, self.next)
         ops = []
         # identical op order on every rank: [send up, send down, recv below, recv above];
         # tags keep the two streams apart when prev == next (2 ranks).
         if send_up is not None:
-            ops.append(d.P2POp(d.isend, send_up, self._g(self.next), self.group, 1))
+            ops.append(d.P2POp(d.isend, send_up, self._g(nxt), self.group, 1))
         if send_down is not None:
-            ops.append(d.P2POp(d.isend, send_down, self._g(self.prev), self.group, 2))
+            ops.append(d.P2POp(d.isend, send_down, self._g(prev), self.group, 2))
         if recv_below is not None:
-            ops.append(d.P2POp(d.irecv, recv_below, self._g(self.prev), self.group, 1))
+            ops.append(d.P2POp(d.irecv, recv_below, self._g(prev), self.group, 1))
         if recv_above is not None:
-            ops.append(d.P2POp(d.irecv, recv_above, self._g(self.next), self.group, 2))
+            ops.append(d.P2POp(d.irecv, recv_above, self._g(nxt), self.group, 2))
         if not ops:
             return None
         return d.batch_isend_irecv(ops)

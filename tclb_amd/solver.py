@@ -149,7 +149,7 @@ class Solver:
                 now = time.time()
                 dt = now - self._meter_t
             mlups = self.lattice.nodes * self._meter_it / dt / 1e6
-            es = 4 if self.lattice.sdtype == torch.float32 else 8
+            es = self.lattice.snaps[0].element_size()
             gbs = mlups * (2 * self.lattice.nf * es + self.lattice.flags.element_size()) / 1e3
             log.output(f"{self.iter:8d} it {mlups:8.1f} MLBUps {gbs:7.2f} GB/s")
             self._meter_t = now

@@ -14,15 +14,16 @@ def setup_flags(lat):
     nx = lat.shape[0]
     fl = np.full((lat.NZ, lat.NY, nx), m.node_type("MRT").value, dtype=np.uint32)
     if m.name == "d3q27":
-        # walls at global y = 0 and y = gny-1 (y not split in 3-D)
-        fl[:, lat.gy + 0, :] = m.node_type("Wall").value
-        fl[:, lat.gy + lat.shape[1] - 1, :] = m.node_type("Wall").value
+        # walls at global y = 0 and y = gny-1 (rows of every local y incl. ghosts)
+        gy = (np.arange(lat.NY) + lat.slab.offset[1] - lat.gy) % lat.gshape[1]
+        fl[:, gy == 0, :] = m.node_type("Wall").value
+        fl[:, gy == lat.gshape[1] - 1, :] = m.node_type("Wall").value
     return fl
 
 
-def run_case(model, shape, steps, comm, overlap=None):
+def run_case(model, shape, steps, comm, overlap=None, grid=None):
     from tclb_amd.lattice import Lattice
-    lat = Lattice(model, shape, comm=comm, overlap=overlap)
+    lat = Lattice(model, shape, comm=comm, overlap=overlap, grid=grid)
     lat.set_flags(setup_flags(lat))
     if model == "d3q27":
         lat.set_setting("nu", 0.05)
@@ -44,19 +45,22 @@ def run_case(model, shape, steps, comm, overlap=None):
     return lat
 
 
-def worker(rank, world, port, model, shape, steps, out, overlap):
+def worker(rank, world, port, model, shape, steps, out, overlap, grid=None):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from tclb_amd.parallel.comm import TorchDistComm
     comm = TorchDistComm()
-    lat = run_case(model, shape, steps, comm, overlap=overlap)
-    parts = comm.gather_objects((lat.slab.lo, lat.fields_interior().numpy(), lat.globals))
+    lat = run_case(model, shape, steps, comm, overlap=overlap, grid=grid)
+    parts = comm.gather_objects((lat.slab.offset, lat.fields_interior().numpy(), lat.globals, lat.slab.axis))
     if rank == 0:
-        axis = 1 if lat.slab.axis == 2 else 2  # concat axis in (nf, z, y, x)
-        parts.sort(key=lambda p: p[0])
-        full = np.concatenate([p[1] for p in parts], axis=axis)
+        gnx, gny, gnz = lat.gshape
+        full = np.zeros((lat.nf, gnz, gny, gnx))
+        for (ox, oy, oz), a, _, _ in parts:
+            full[:, oz:oz + a.shape[1], oy:oy + a.shape[2], :] = a
         np.save(out, full)
+        with open(out + ".axis", "w") as f:
+            f.write(str(parts[0][3]))
         import json
         with open(out + ".json", "w") as f:
             json.dump(parts[0][2], f)

@@ -38,3 +38,33 @@ def test_ranks_match_single(tmp_path, model, shape, world, overlap):
     g = json.load(open(out + ".json"))
     for k, v in ref.globals.items():
         assert abs(g[k] - v) <= 1e-11 * (1 + abs(v)), k
+
+
+@pytest.mark.parametrize("shape,world,grid", [
+    ((16, 8, 12), 4, (2, 2)),      # explicit Y x Z grid
+    ((12, 9, 8), 6, (3, 2)),
+    ((8, 6, 3), 4, None),          # z too thin for 4 slabs: automatic Y x Z fallback
+])
+def test_yz_grid_matches_single(tmp_path, shape, world, grid):
+    """reference MPIDivision (src/Solver.cpp.Rt:288-370): a Y x Z process grid with
+    two-phase halos (z planes, then y rows incl. the z ghosts = edge ghosts) reproduces
+    one rank bit-for-bit, corners included (d3q27 reads all 26 neighbours)"""
+    steps = 4
+    ref = dist_worker.run_case("d3q27", shape, steps, LoopbackComm())
+    out = str(tmp_path / "full.npy")
+    mp.start_processes(dist_worker.worker, args=(world, _port(), "d3q27", shape, steps, out, None, grid),
+                       nprocs=world, start_method="spawn", join=True)
+    assert open(out + ".axis").read() == "3"
+    full = np.load(out)
+    assert np.array_equal(full, ref.fields_interior().numpy())
+    g = json.load(open(out + ".json"))
+    for k, v in ref.globals.items():
+        assert abs(g[k] - v) <= 1e-11 * (1 + abs(v)), k
+
+
+def test_choose_grid_minimises_cut():
+    from tclb_amd.parallel.decomp import choose_grid, decompose
+    assert choose_grid(512, 512, 512, 8) in ((2, 4), (4, 2))
+    assert choose_grid(1280, 130, 130, 16) == (4, 4)
+    s = decompose(64, 32, 32, 5, 64)         # 32 z planes cannot hold 64 slabs
+    assert s.axis == 3 and (s.py, s.pz) == (8, 8) and (s.ry, s.rz) == (5, 0)

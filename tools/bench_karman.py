@@ -37,7 +37,7 @@ CASE = """<CLBConfig version="2.0" output="{out}/" permissive="true">
   <Param name="VelocityX" value="0.01"/>
   <Param name="Viscosity" value="0.02"/>
  </Model>
- <VTK Iterations="{vtk}"/>
+ {vtk}
  <Solve Iterations="{iters}"/>
 </CLBConfig>
 """
@@ -48,6 +48,7 @@ def main():
     ap.add_argument("--iters", type=int, default=10000)
     ap.add_argument("--vtk", type=int, default=1000)
     ap.add_argument("--device", default=None)
+    ap.add_argument("--precision", default="double")
     a = ap.parse_args()
     import io
     import contextlib
@@ -55,11 +56,12 @@ def main():
     from tclb_amd import handlers  # noqa: F401
     from tclb_amd.solver import Solver
     out = tempfile.mkdtemp(prefix="karman_")
-    root = ET.fromstring(CASE.format(out=out, iters=a.iters, vtk=a.vtk))
+    vtk = f'<VTK Iterations="{a.vtk}"/>' if a.vtk > 0 else ""      # --vtk 0: compute only
+    root = ET.fromstring(CASE.format(out=out, iters=a.iters, vtk=vtk))
     dev = a.device or ("cuda" if torch.cuda.is_available() else "cpu")
     buf = io.StringIO()
     with contextlib.redirect_stdout(buf), contextlib.redirect_stderr(buf):
-        s = Solver("d2q9", root, conffile=os.path.join(out, "karman.xml"), device=dev)
+        s = Solver("d2q9", root, conffile=os.path.join(out, "karman.xml"), device=dev, precision=a.precision)
         t0 = time.perf_counter()
         s.run()
         if dev == "cuda":
@@ -68,7 +70,7 @@ def main():
     log = buf.getvalue()
     meter = [float(v) for v in re.findall(r"([0-9.]+) MLBUps", log)]
     nodes = 1024 * 100
-    print(json.dumps({"case": "karman d2q9 1024x100", "device": dev, "iters": a.iters,
+    print(json.dumps({"case": "karman d2q9 1024x100", "device": dev, "precision": a.precision, "vtk_every": a.vtk, "iters": a.iters,
                       "wall_s": round(dt, 3), "MLUPS_whole_run": round(nodes * a.iters / dt / 1e6, 1),
                       "meter_MLBUps_max": max(meter) if meter else None,
                       "vtk_files": len([f for f in os.listdir(out) if f.endswith(".vti")])}), flush=True)
