@@ -1,8 +1,10 @@
 """Discrete adjoint of the lattice time stepping (reference: Lattice::Iteration_Adj,
 IterateTill and the snapshot hierarchy, src/Lattice.cu.Rt:46-61,542-613,843-890).
 
-Every model is differentiable: the AD executor (csrc/include/tclb/executor_ad.hpp)
-re-runs a stage with dual numbers and applies the transposed local Jacobian.  This module
+Every model is differentiable: the AD executor re-runs a stage with dual numbers and
+applies the transposed local Jacobian — on the CPU (csrc/include/tclb/executor_ad.hpp,
+OpenMP) or on the GPU (csrc/include/tclb_ad/executor_ad_hip.hpp: windowed tangents,
+device fp64 atomics for the adjoint push), following the lattice's device.  This module
 drives it over actions (reverse stage order, in-place stages pass the adjoint of the
 fields they do not write through), folds ghost-plane contributions back to their owners,
 and runs unsteady adjoints with checkpointed recomputation of the primal trajectory.
@@ -31,22 +33,24 @@ class AdjointError(RuntimeError):
 
 class Adjoint:
     def __init__(self, lat, settings: Sequence[str] = (), zonal: Sequence[str] = ()):
-        if lat.is_gpu:
-            raise AdjointError("the adjoint executor runs on the CPU lattice (device='cpu')")
         if lat.comm.size > 1:
             raise AdjointError("adjoint runs are single-rank")
         if lat.sdtype != torch.float64:
             raise AdjointError("adjoint needs double precision storage")
         self.lat = lat
-        self.lib = abi.load_ad(lat.model.name)
-        m = lat.model
-        self.set_mask = np.array([1 if s in settings else 0 for s in lat.gsettings] or [0], dtype=np.int32)
-        self.zon_mask = np.array([1 if s in zonal else 0 for s in lat.zsettings] or [0], dtype=np.int32)
-        self.gset = np.zeros(max(1, len(lat.gsettings)), dtype=np.float64)
-        self.gzon = np.zeros(lat.zvals.size if lat.zvals.size else 1, dtype=np.float64)
+        self.lib = abi.load_ad(lat.model.name, gpu=lat.is_gpu)
+        dev = lat.device
+        self.set_mask = torch.tensor([1 if s in settings else 0 for s in lat.gsettings] or [0], dtype=torch.int32,
+                                     device=dev)
+        self.zon_mask = torch.tensor([1 if s in zonal else 0 for s in lat.zsettings] or [0], dtype=torch.int32,
+                                     device=dev)
+        self.gset = torch.zeros(max(1, len(lat.gsettings)), dtype=torch.float64, device=dev)
+        self.gzon = torch.zeros(lat.zvals.size if lat.zvals.size else 1, dtype=torch.float64, device=dev)
         self.scratch = torch.zeros_like(lat.snaps[0])
         self.series_grads = {}
         self.ctx = abi.AdCtx()
+        # the GPU executor reads its context from device memory
+        self._ctx_dev = torch.zeros(ctypes.sizeof(abi.AdCtx), dtype=torch.uint8, device=dev) if lat.is_gpu else None
 
     # ------------------------------------------------------------------ one action
     def _fold_ghosts(self, a: torch.Tensor):
@@ -84,13 +88,19 @@ class Adjoint:
         c = self.ctx
         c.aout = aout.data_ptr()
         c.ain = ain.data_ptr()
-        c.gset = self.gset.ctypes.data
-        c.gzon = self.gzon.ctypes.data
-        c.set_mask = self.set_mask.ctypes.data
-        c.zon_mask = self.zon_mask.ctypes.data
+        c.gset = self.gset.data_ptr()
+        c.gzon = self.gzon.data_ptr()
+        c.set_mask = self.set_mask.data_ptr()
+        c.zon_mask = self.zon_mask.data_ptr()
         c.obj_weight = obj_weight
         c.overflow = 0
-        L.ext[5] = ctypes.cast(ctypes.pointer(c), ctypes.c_void_p)
+        L.reserved2 = 0
+        L.stream = lat._stream()
+        if self._ctx_dev is not None:
+            self._ctx_dev.copy_(torch.frombuffer(bytearray(bytes(c)), dtype=torch.uint8))
+            L.ext[5] = self._ctx_dev.data_ptr()
+        else:
+            L.ext[5] = ctypes.cast(ctypes.pointer(c), ctypes.c_void_p)
         if lat.turb_t is not None:
             L.ext[0] = lat.turb_t.data_ptr()
             L.next[0] = lat.turb_t.shape[0]
@@ -99,6 +109,8 @@ class Adjoint:
             L.ext[1] = lat.cuts.data_ptr()
             L.next[1] = lat.cuts.numel()
         self.lib.run(L)
+        if self._ctx_dev is not None:
+            c = abi.AdCtx.from_buffer_copy(bytes(self._ctx_dev.cpu().numpy()))
         if c.overflow:
             raise AdjointError(f"model {lat.model.name}: a node needed more than {self.lib.tangents} AD tangents")
         self._fold_ghosts(ain)
@@ -170,7 +182,7 @@ class Adjoint:
             lat.iter = it0 + t
             if lat.zseries:
                 lat.apply_series()
-                before = self.gzon.copy()
+                before = self.gzon.cpu().numpy().copy()
             a = self.step_back(a, action)
             if lat.zseries:
                 self._series_grad(before, lat)
@@ -185,7 +197,7 @@ class Adjoint:
         """attribute this reverse step's zonal-setting gradient to the active entry of
         each zonal time series (reference zSet gradient tables per time index)"""
         nz = lat.zvals.shape[1]
-        d = self.gzon - before
+        d = self.gzon.cpu().numpy() - before
         for key, v in lat.zseries.items():
             g = self.series_grads.setdefault(key, np.zeros(len(v)))
             g[lat.series_index(key)] += d[key[0] * nz + key[1]]
@@ -195,13 +207,27 @@ class Adjoint:
         key = (lat.zsettings.index(name), lat.zone_index(zone or "DefaultZone"))
         return self.series_grads.get(key, np.zeros(len(lat.zseries.get(key, [0.0])))).copy()
 
+    def param_fields(self) -> List[int]:
+        return [i for i, f in enumerate(self.lat.model.fields) if f.parameter]
+
+    def steady_step(self, a: torch.Tensor, action: str = "Iteration") -> torch.Tensor:
+        """one steady-adjoint iteration (reference SteadyAdjoint kernels, "SAdj" dispatch
+        with zeropar, src/conf.R:831-839): the adjoint of the parameter densities is
+        zeroed on entry, so on exit it holds this iteration's gradient contribution
+        lambda^T dF/dp + dJ/dp — the steady design gradient once lambda has converged"""
+        a = a.clone()
+        pf = self.param_fields()
+        if pf:
+            a[pf] = 0
+        self.gset.zero_()
+        self.gzon.zero_()
+        return self.step_back(a, action)
+
     def steady(self, iterations: int, action: str = "Iteration", tol: float = 0.0) -> torch.Tensor:
         """fixed-point adjoint at the current (converged) primal state: a <- A^T a + dJ/df"""
         a = torch.zeros_like(self.lat.snaps[self.lat.cur])
         for _ in range(iterations):
-            self.gset[:] = 0
-            self.gzon[:] = 0
-            b = self.step_back(a, action)
+            b = self.steady_step(a, action)
             d = float((b - a).abs().max())
             a = b
             if tol and d < tol:
@@ -216,7 +242,7 @@ class Adjoint:
         lat = self.lat
         i = lat.model.field_index(name)
         nx, ny, nz = lat.shape
-        return self.a0[i, lat.gz:lat.gz + nz, lat.gy:lat.gy + ny, :nx].numpy().copy()
+        return self.a0[i, lat.gz:lat.gz + nz, lat.gy:lat.gy + ny, :nx].cpu().numpy().copy()
 
     def setting_gradient(self, name: str, zone: Optional[str] = None) -> float:
         lat = self.lat

@@ -14,6 +14,7 @@ import os
 import shutil
 import subprocess
 import sys
+import threading
 import time
 from concurrent.futures import ThreadPoolExecutor
 from typing import Dict, Iterable, List, Optional
@@ -56,7 +57,8 @@ def _hash_inputs(paths: Iterable[str], extra: str = "") -> str:
 def _deps(model_dir: str, dynamics: Optional[str]) -> List[str]:
     inc = os.path.join(CSRC, "include", "tclb")
     deps = [os.path.join(inc, f) for f in os.listdir(inc) if f.endswith((".hpp", ".h"))]
-    deps += [os.path.join(model_dir, f) for f in os.listdir(model_dir) if f.endswith((".hpp", ".hip", ".cpp"))]
+    deps += [os.path.join(model_dir, f) for f in os.listdir(model_dir)
+             if f.endswith((".hpp", ".hip", ".cpp")) and f != "kernels_adhip.hip"]
     # the dynamics include and everything it includes from csrc/models (transitively)
     todo = [dynamics] if dynamics else []
     seen = set()
@@ -75,8 +77,31 @@ def _deps(model_dir: str, dynamics: Optional[str]) -> List[str]:
     return deps
 
 
+AD_HIP_DIR = os.path.join(CSRC, "include", "tclb_ad")
+
+
+def _adhip_source(model, gen_dir: str) -> str:
+    """GPU adjoint executor instantiation (csrc/include/tclb_ad/executor_ad_hip.hpp),
+    written next to the emitted model header"""
+    from .emit.emitter import ad_tangents
+    m = model.finalize()
+    src = (f"// AUTO-GENERATED: GPU adjoint (AD) executor for model {m.name}\n"
+           f"#define TCLB_AD_K {ad_tangents(m)}\n"
+           f'#include "model.hpp"\n'
+           f'#include "tclb_ad/executor_ad_hip.hpp"\n'
+           f"TCLB_EXPORT_AD_HIP({m.name}, tclb::M_{m.name}::Model)\n")
+    p = os.path.join(gen_dir, "kernels_adhip.hip")
+    if not os.path.exists(p) or open(p).read() != src:
+        with open(p, "w") as f:
+            f.write(src)
+    return p
+
+
 def _cmd(kind: str, src: str, out: str, gen_dir: str, variant: str = "") -> List[str]:
     incs = ["-I", os.path.join(CSRC, "include"), "-I", os.path.join(CSRC, "models"), "-I", gen_dir]
+    if kind == "adhip":
+        return [HIPCC, f"--offload-arch={ARCH}", "-O2", "-std=c++17", "-fPIC", "-shared", "-munsafe-fp-atomics",
+                "-Wno-unused-result", "-Wno-pass-failed", *incs, src, "-o", out]
     if kind == "hip":
         # simplifycfg-sink-common=false: boundary-condition switch cases that permute
         # the population array differ only in constant indices; sinking them into one
@@ -127,7 +152,12 @@ def source_stamp(name: str, kind: str, variant: str = "") -> str:
     gdir = os.path.join(BUILD, "gen", name)
     v = variant if kind == "hip" else ""
     cmd = _cmd(kind, os.path.join(gdir, "kernels_" + kind), lib_path(name, kind, v), gdir, v)
-    return _rel_hash(_deps_no_gen(model.dynamics), " ".join(cmd) + _python_stamp())
+    deps = _deps_no_gen(model.dynamics) + (_ad_hip_deps() if kind == "adhip" else [])
+    return _rel_hash(deps, " ".join(cmd) + _python_stamp())
+
+
+def _ad_hip_deps() -> List[str]:
+    return [os.path.join(AD_HIP_DIR, f) for f in sorted(os.listdir(AD_HIP_DIR)) if f.endswith(".hpp")]
 
 
 def _deps_no_gen(dynamics: Optional[str]) -> List[str]:
@@ -168,20 +198,21 @@ def build_model(name: str, kinds=("cpu", "hip"), force: bool = False, verbose: b
     os.makedirs(LIB, exist_ok=True)
     out = {}
     for kind in kinds:
-        if kind == "hip" and not os.path.exists(HIPCC):
+        if kind in ("hip", "adhip") and not os.path.exists(HIPCC):
             continue
         v = variant if kind == "hip" else ""
         target = lib_path(name, kind, v)
-        src = paths[kind]
+        src = _adhip_source(model, paths["dir"]) if kind == "adhip" else paths[kind]
         cmd = _cmd(kind, src, target, paths["dir"], v)
-        h = _hash_inputs(_deps(paths["dir"], model.dynamics), " ".join(cmd))
+        deps = _deps(paths["dir"], model.dynamics) + (_ad_hip_deps() if kind == "adhip" else [])
+        h = _hash_inputs(deps, " ".join(cmd))
         stamp = target + ".hash"
         if not force and os.path.exists(target) and os.path.exists(stamp) and open(stamp).read() == h:
             _write_src_stamp(name, kind, variant)
             out[kind] = target
             continue
         t0 = time.time()
-        tmp = target + ".tmp"
+        tmp = f"{target}.{os.getpid()}.{threading.get_ident()}.tmp"
         cmd[-1] = tmp
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:

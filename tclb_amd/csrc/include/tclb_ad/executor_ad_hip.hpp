@@ -1,0 +1,138 @@
+// Adjoint (reverse) executor on the GPU (gfx950).  Same scheme as the CPU executor
+// (csrc/include/tclb/executor_ad.hpp): every node update is re-run with dual numbers,
+// the local Jacobian is contracted with the adjoint of the stage outputs and scattered to
+// the adjoint of the loaded inputs with device fp64 atomics — the reference's adjoint
+// push (src/LatticeAccess.inc.cpp.Rt:349-361, Tapenade Run_b kernels, src/Lattice.cu.Rt
+// :542-613).
+//
+// GPU shape: a node reads up to TCLB_AD_K distinct inputs (populations, stencil fields,
+// seeded settings), but carrying K tangents per value would put every value of the node
+// code in scratch (K+1 doubles each).  Instead each thread re-runs its node in passes of
+// TCLB_AD_WINDOW tangents: pass p seeds only the inputs whose first-read index falls in
+// [p W, (p+1) W).  The first-read order is the same in every pass (identical primal
+// values, identical branches), so the passes partition the Jacobian columns; the thread
+// stops after the pass that covers the last input it saw.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <utility>
+#include "tclb/ad.hpp"
+
+#ifndef TCLB_AD_WINDOW
+#define TCLB_AD_WINDOW 4
+#endif
+
+namespace tclb {
+
+template <class T, int C>
+struct AdRec<Dual<T, C>> {
+  static constexpr int KMAX = TCLB_AD_K;
+  typedef Dual<T, C> D;
+  AdCtx* ctx;
+  long long fs, zp;
+  int n, base;
+  long long key[KMAX];   // first-read order of the inputs: kind<<60 | field<<44 | index
+  TCLB_FN void init(const Launch& L) {
+    ctx = (AdCtx*)L.ext[5];
+    fs = L.fs;
+    zp = L.nzones;
+    n = 0;
+    base = L.reserved2;
+  }
+  TCLB_FN static long long mk(int kind, int f, long long i) {
+    return ((long long)kind << 60) | ((long long)f << 44) | i;
+  }
+  TCLB_FN D mark(double v, int j) const {
+    D r(v);
+    if (j >= base && j < base + C) r.d[j - base] = T(1);
+    return r;
+  }
+  TCLB_FN int find(long long k) const {
+    for (int j = 0; j < n; j++)
+      if (key[j] == k) return j;
+    return -1;
+  }
+  TCLB_FN D seed(double v, long long k) {
+    const int j = find(k);
+    if (j >= 0) return mark(v, j);
+    if (n < KMAX) {
+      key[n] = k;
+      return mark(v, n++);
+    }
+    ctx->overflow = 1;
+    return D(v);
+  }
+  TCLB_FN D load(double v, int f, long long i) { return ctx ? seed(v, mk(0, f, i)) : D(v); }
+  TCLB_FN D setting(int i, D v) {
+    return (ctx && ctx->set_mask && ctx->set_mask[i]) ? seed(v.v, mk(1, i, 0)) : v;
+  }
+  TCLB_FN D zonal(int i, int zone, D v) {
+    return (ctx && ctx->zon_mask && ctx->zon_mask[i]) ? seed(v.v, mk(2, i, zone)) : v;
+  }
+  TCLB_FN void scatter(double a, const D& val) {
+    if (a == 0.0) return;
+    for (int c = 0; c < C; c++) {
+      const int j = base + c;
+      if (j >= n) break;
+      const double d = a * (double)val.d[c];
+      if (d == 0.0) continue;
+      const long long k = key[j];
+      const int kind = (int)(k >> 60), f = (int)((k >> 44) & 0xffff);
+      const long long i = k & ((1LL << 44) - 1);
+      double* dst = kind == 0 ? ctx->ain + (long long)f * fs + i
+                              : (kind == 1 ? ctx->gset + f : ctx->gzon + (long long)f * zp + i);
+      unsafeAtomicAdd(dst, d);
+    }
+  }
+  TCLB_FN void store(int f, long long node, const D& val) {
+    if (ctx) scatter(ctx->aout[(long long)f * fs + node], val);
+  }
+};
+
+namespace exec {
+
+template <class Model, int STG>
+__global__ void __launch_bounds__(64) k_ad(const Launch L, AdCtx* ctx) {
+  typedef Dual<double, TCLB_AD_WINDOW> D;
+  constexpr int NG = Model::NGLOBALS_;
+  constexpr int NSUM = Model::NSUMGLOBALS_;
+  const int x = L.xlo + (int)(blockIdx.x * blockDim.x + threadIdx.x);
+  const int y = L.ylo + (int)blockIdx.y;
+  const int z = L.zlo + (int)blockIdx.z;
+  if (x >= L.xhi) return;
+  Launch L2 = L;
+  L2.ext[5] = ctx;
+  for (int base = 0; base < TCLB_AD_K; base += TCLB_AD_WINDOW) {
+    L2.reserved2 = base;
+    D g[NG];
+    for (int i = 0; i < NG; i++) g[i] = i < NSUM ? D(0.0) : D(-1e30);
+    typename Model::template NodeT<D, double, true> nd(L2, x, y, z, g);
+    nd.template run_stage<STG>();
+    if (ctx->obj_weight != 0.0) nd.ad_.scatter(ctx->obj_weight, g[Model::OBJ_]);
+    if (base + TCLB_AD_WINDOW >= nd.ad_.n) break;   // every input seen has had its pass
+  }
+}
+
+template <class Model, int... I>
+inline int ad_hip_impl(const Launch& L, AdCtx* ctx, std::integer_sequence<int, I...>) {
+  const int w = L.xhi - L.xlo, h = L.yhi - L.ylo, d = L.zhi - L.zlo;
+  if (w <= 0 || h <= 0 || d <= 0) return 0;
+  const dim3 grid((w + 63) / 64, h, d), block(64, 1, 1);
+  hipStream_t s = (hipStream_t)L.stream;
+  bool found = false;
+  ((L.stage == I ? (k_ad<Model, I><<<grid, block, 0, s>>>(L, ctx), found = true) : false), ...);
+  if (!found) return -2;
+  return (int)hipGetLastError();
+}
+
+}  // namespace exec
+}  // namespace tclb
+
+// ctx: device copy of the AdCtx (aout/ain/gset/gzon/masks are device pointers)
+#define TCLB_EXPORT_AD_HIP(NAME, MODEL)                                                      \
+  extern "C" int tclb_##NAME##_adjoint(const tclb::Launch* L) {                              \
+    return tclb::exec::ad_hip_impl<MODEL>(*L, (tclb::AdCtx*)L->ext[5],                       \
+                                          std::make_integer_sequence<int, MODEL::NSTAGES_>{}); \
+  }                                                                                          \
+  extern "C" int tclb_##NAME##_ad_tangents() { return TCLB_AD_K; }                           \
+  extern "C" int tclb_##NAME##_ad_device() { return 1; }                                     \
+  extern "C" int tclb_##NAME##_sizeof_launch() { return (int)sizeof(tclb::Launch); }

@@ -14,6 +14,7 @@ import math
 from typing import List
 
 import numpy as np
+import torch
 
 from ..utils.log import log
 from .base import (HANDLER_DESIGN, Action, Design, GenericAction, HandlerError, register)
@@ -664,22 +665,29 @@ class FDTest(_Optimizer):
 
 
 @register("OptSolve")
-class OptSolve(_Optimizer):
-    """simple steepest ascent with step Descent (reference acOptSolve / ITER_OPT):
-    repeat Iterations times: run the children (with an Adjoint), move the parameters
-    by Descent * gradient within their bounds"""
+class OptSolve(GenericAction):
+    """one-shot optimisation loop (reference acOptSolve, src/Handlers/acOptSolve.cpp:5-40):
+    a Solve whose iterations are ITER_OPT iterations — primal step, one steady-adjoint
+    step, then the design update p += Descent * dJ/dp on DesignSpace nodes (clamped to
+    [0, 1]) — until Iterations, with the callbacks of the enclosing level firing as in
+    <Solve>.  The adjoint state is carried from iteration to iteration."""
 
     def init(self):
         super().init()
-        x, lo, hi = self._prepare()
-        steps = int(float(self.node.get("Iterations", "10")))
-        descent = float(self.node.get("Descent", str(self.solver.lattice.get_setting("Descent")
-                                                      if "Descent" in self.solver.lattice.gsettings else 1e-3)))
-        for _ in range(steps):
-            J, g = self._evaluate(x)
-            x = np.clip(x + descent * g, lo, hi)
-        self.solver.lattice.snaps[self.solver.lattice.cur].copy_(self.state0)
-        _set_all(self.solver, x)
+        from ..adjoint import Adjoint
+        from ..solver import ITER_OPT
+        s = self.solver
+        lat = s.lattice
+        old = s.iter_type
+        self.execute_internal()
+        s.opt_adjoint = Adjoint(lat)
+        s.opt_state = torch.zeros_like(lat.snaps[lat.cur])
+        s.iter_type = old | ITER_OPT
+        try:
+            self.solve_loop()
+        finally:
+            s.iter_type = old
+        self.unstack()
         return 0
 
 

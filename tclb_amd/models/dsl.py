@@ -306,6 +306,8 @@ class Model:
             self.add_setting(f"{g.name}InObj", default=0.0, zonal=True,
                              comment=f"Weight of [{g.comment or g.name}] in objective", preload=False)
         self.add_setting("Threshold", default=0.5, comment="Parameters threshold")
+        if self.setting("Descent") is None:   # reference src/conf.R:735 (ITER_OPT step)
+            self.add_setting("Descent", default=0.0, comment="Optimization Descent")
         autosym = int(self.options.get("autosym", 0) or 0)
         if autosym:   # automatic symmetry node types (src/conf.R:440-457)
             nm = "Symmetry" if autosym == 1 else "SymmetryEdge"

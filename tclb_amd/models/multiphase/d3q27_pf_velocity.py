@@ -9,7 +9,13 @@ Boundary.c.Rt, thermocapillary.R, thermo.c.Rt}.  Implemented options: ``q27``, `
 ``thermo`` (temperature field by explicit RK4 with phase-dependent conductivity and heat
 capacity; surface tension sigma(T) enters the chemical potential and a Marangoni force),
 ``planarBenchmark`` (heated-wall layered benchmark initialisation, with ``thermo``) and
-``autosym`` (1/2); geometric, staircaseimp, isograd and tprec are not built yet.
+``autosym`` (1/2), and the wetting-boundary options of Boundary.c.Rt: ``geometric``
+(geometric contact-angle condition from the tangential phase gradient extrapolated from
+two nodes along the wall normal, with the gradient stages calcPhaseGrad[_init]),
+``staircaseimp`` (the wall normal is the exact surface normal, extended to the D3Q27 cube
+surface; values along it are interpolated barycentrically on the hit triangle of the cube
+face), ``isograd`` (isotropic gradients near walls from the previous iteration) and
+``tprec`` (a second, smaller triangle for the second interpolation point).
 
 Build-time derivations (sympy, replacing the reference's R polynomial algebra):
 * the 27x27 moment matrix M factorises as M = C . Mraw, Mraw the raw-monomial
@@ -66,7 +72,12 @@ def _bounce(U):
 
 
 def build(q27: bool = False, bgk: bool = False, thermo: bool = False, planarbenchmark: bool = False,
-          outflow: bool = False, autosym: int = 0) -> Model:
+          outflow: bool = False, autosym: int = 0, geometric: bool = False, staircaseimp: bool = False,
+          isograd: bool = False, tprec: bool = False) -> Model:
+    if thermo and geometric:
+        # Dynamics.R:155-169: with thermo the actions use the surface-energy stages
+        # (WallInit, calcWall), which geometric renames to *_CA: no buildable variant
+        raise NotImplementedError("thermo with geometric has no actions in the reference (Dynamics.R:155-169)")
     m = Model("d3q27_pf_velocity", dims=3, family="multiphase", reference="models/multiphase/d3q27_pf_velocity",
               description="phase-field (D3Q15/D3Q27 h) + velocity-based hydrodynamics (D3Q27 g), "
                           "weighted-MRT, high density ratio")
@@ -78,10 +89,27 @@ def build(q27: bool = False, bgk: bool = False, thermo: bool = False, planarbenc
         m.add_density(n, 0, 0, 0, group="Vel")
     for n in ("nw_x", "nw_y", "nw_z"):
         m.add_density(n, 0, 0, 0, group="nw")
+    extra_save, extra_load, extra_phase, extra_bc = [], [], [], []
+    if staircaseimp:        # Dynamics.R:36-61
+        for n in ("nw_actual_x", "nw_actual_y", "nw_actual_z"):
+            m.add_density(n, 0, 0, 0, group="nw_actual")
+        for n in ("coeff_v1", "coeff_v2", "coeff_v3", "triangle_index"):
+            m.add_density(n, 0, 0, 0, group="st_interpolation")
+        if tprec:
+            for n in ("coeff2_v1", "coeff2_v2", "coeff2_v3", "triangle_index2"):
+                m.add_density(n, 0, 0, 0, group="st_interpolation")
+        extra_save = ["nw_actual", "st_interpolation"]
+        extra_load = ["nw_actual", "st_interpolation"]
+        extra_phase = ["nw_actual"]
+        extra_bc = ["nw_actual", "st_interpolation"]
     m.add_density("IsSpecialBoundaryPoint", 0, 0, 0, group="solid_boundary")
     m.add_quantity("SpecialBoundaryPoint", unit="1")
-    m.add_field("IsBoundary", stencil3d=1, group="solid_boundary")
-    m.add_field("PhaseF", stencil3d=1, group="PF")
+    m.add_field("IsBoundary", stencil3d=2 if geometric else 1, group="solid_boundary")
+    if geometric:           # Dynamics.R:93-109: gradients read two nodes along the normal
+        for n in ("gradPhiVal_x", "gradPhiVal_y", "gradPhiVal_z"):
+            m.add_field(n, stencil3d=2, group="gradPhi")
+        m.add_field("gradPhi_PhaseF", stencil3d=1, group="gradPhi")
+    m.add_field("PhaseF", stencil3d=2 if geometric else 1, group="PF")
     for i, u in enumerate(U27):
         m.add_density(f"g[{i}]", int(u[0]), int(u[1]), int(u[2]), group="g")
     for i, u in enumerate(U27[:Qh]):
@@ -89,9 +117,9 @@ def build(q27: bool = False, bgk: bool = False, thermo: bool = False, planarbenc
 
     save_initial_PF = ["PF", "Vel"]
     save_initial = ["g", "h", "PF"]
-    save_iteration = ["g", "h", "Vel", "nw", "solid_boundary"]
-    load_iteration = ["g", "h", "Vel", "nw", "solid_boundary"]
-    load_phase = ["g", "h", "Vel", "nw", "solid_boundary"]
+    save_iteration = ["g", "h", "Vel", "nw", "solid_boundary"] + extra_save
+    load_iteration = ["g", "h", "Vel", "nw", "solid_boundary"] + extra_load
+    load_phase = ["g", "h", "Vel", "nw", "solid_boundary"] + extra_phase
     if outflow:
         # Dynamics.R:65-79 + lattice.R:63-66: every density readable one node east/west of
         # its pull location (Neumann / convective outflow), U readable at x+-1, and the
@@ -118,8 +146,18 @@ def build(q27: bool = False, bgk: bool = False, thermo: bool = False, planarbenc
     m.add_stage("calcPhase", "calcPhaseF", save_fields=["PhaseF"], load_densities=load_phase)
     m.add_stage("BaseIter", "Run", save_fields=save_iteration, load_densities=load_iteration)
     m.add_stage("InitFromFieldsStage", "InitFromFieldsStage", save_fields=save_initial_PF, load_densities=["init"])
-    m.add_stage("WallInit", "Init_wallNorm", save_fields=["nw", "solid_boundary"])
-    m.add_stage("calcWall", "calcWallPhase", save_fields=["PhaseF"], load_densities=["nw", "solid_boundary"])
+    if geometric:           # Dynamics.R:129-135
+        m.add_stage("WallInit_CA", "Init_wallNorm", save_fields=["nw", "solid_boundary"] + extra_bc)
+        m.add_stage("calcWall_CA", "calcWallPhase", save_fields=["PhaseF"],
+                    load_densities=["nw", "gradPhi", "PF", "solid_boundary"] + extra_bc)
+        m.add_stage("calcPhaseGrad", "calcPhaseGrad", save_fields=["gradPhi"],
+                    load_densities=["nw", "PF", "solid_boundary"])
+        m.add_stage("calcPhaseGrad_init", "calcPhaseGrad_init", save_fields=["gradPhi"],
+                    load_densities=["nw", "PF", "solid_boundary"])
+    else:
+        m.add_stage("WallInit", "Init_wallNorm", save_fields=["nw", "solid_boundary"] + extra_bc)
+        m.add_stage("calcWall", "calcWallPhase", save_fields=["PhaseF"],
+                    load_densities=["nw", "solid_boundary"] + extra_bc)
     m.add_stage("calcWallPhase_correction", "calcWallPhase_correction", save_fields=["PhaseF"],
                 load_densities=["nw", "solid_boundary"])
     if thermo:
@@ -140,6 +178,13 @@ def build(q27: bool = False, bgk: bool = False, thermo: bool = False, planarbenc
         m.add_action("Iteration", ["BaseIter", "calcPhase", "calcWall"] + rk)
         m.add_action("IterationConstantTemp", ["BaseIter", "calcPhase", "calcWall", "CopyThermal"])
         m.add_action("Init", ["PhaseInit", "WallInit", "calcWall", "BaseInit"])
+    elif geometric:         # Dynamics.R:160-164
+        grad = "calcPhaseGrad" if isograd else "calcPhaseGrad_init"
+        m.add_action("Iteration", ["BaseIter", "calcPhase", grad, "calcWall_CA", "calcWallPhase_correction"])
+        m.add_action("Init", ["PhaseInit", "WallInit_CA", "calcPhaseGrad_init", "calcWall_CA",
+                              "calcWallPhase_correction", "BaseInit"])
+        m.add_action("InitFields", ["InitFromFieldsStage", "WallInit_CA", "calcPhaseGrad_init", "calcWall_CA",
+                                    "calcWallPhase_correction", "BaseInit"])
     else:
         m.add_action("Iteration", ["BaseIter", "calcPhase", "calcWall", "calcWallPhase_correction"])
         m.add_action("Init", ["PhaseInit", "WallInit", "calcWall", "calcWallPhase_correction", "BaseInit"])
@@ -153,6 +198,10 @@ def build(q27: bool = False, bgk: bool = False, thermo: bool = False, planarbenc
     m.add_quantity("Pstar", unit="1")
     m.add_quantity("Normal", unit="1", vector=True)
     m.add_quantity("IsItBoundary", unit="1")
+    if geometric:
+        m.add_quantity("GradPhi", unit="1", vector=True)
+    if staircaseimp:
+        m.add_quantity("ActualNormal", unit="1", vector=True)
     # ---- settings (Dynamics.R:185-245)
     S = m.add_setting
     S("Density_h", comment="High density")
@@ -237,8 +286,8 @@ def build(q27: bool = False, bgk: bool = False, thermo: bool = False, planarbenc
                  ("LiqTotalPhase", "1"), ("FluxNodeCount", "1"), ("FluxX", "1"), ("FluxY", "1"), ("FluxZ", "1")]:
         m.add_global(g, unit=u)
     m.options = {"q27": q27, "BGK": bgk, "OutFlow": outflow, "thermo": thermo,
-                 "planarBenchmark": planarbenchmark, "autosym": autosym, "geometric": False,
-                 "staircaseimp": False, "isograd": False, "tprec": False}
+                 "planarBenchmark": planarbenchmark, "autosym": autosym, "geometric": geometric,
+                 "staircaseimp": staircaseimp, "isograd": isograd, "tprec": tprec}
     m.defines["hPops"] = str(Qh)
     m.add_codegen(lambda _m: codegen(Qh))
     m.add_codegen(_field_index_block)

@@ -100,7 +100,18 @@ def variant_status(name: str) -> str:
         miss = _missing_kwargs(*r)
     except ModuleNotFoundError:
         return "not implemented: model module " + r[0]
-    return "ok" if not miss else "not implemented: " + ", ".join(miss)
+    if miss:
+        return "not implemented: " + ", ".join(miss)
+    bad = _INVALID.get(r[0], lambda kw: None)(r[2])
+    return "not buildable: " + bad if bad else "ok"
+
+
+# option combinations the reference itself cannot build (module -> kwargs -> reason)
+_INVALID = {
+    ".multiphase.d3q27_pf_velocity": lambda kw: ("thermo with geometric (the thermo actions use the "
+                                                 "surface-energy stages, Dynamics.R:155-169)")
+    if kw.get("thermo") and kw.get("geometric") else None,
+}
 
 
 _cache: Dict[str, Model] = {}

@@ -103,10 +103,12 @@ class AdCtx(ctypes.Structure):
 
 
 class AdLib:
-    """the adjoint (AD) executor library of one model: libtclb_<model>_ad.so"""
+    """the adjoint (AD) executor library of one model: libtclb_<model>_ad.so (CPU) or
+    libtclb_<model>_adhip.so (GPU, tclb_ad/executor_ad_hip.hpp)"""
 
-    def __init__(self, model: str, path: str):
+    def __init__(self, model: str, path: str, kind: str = "ad"):
         self.model = model
+        self.kind = kind
         self.lib = ctypes.CDLL(path, mode=ctypes.RTLD_LOCAL)
         self._adj = getattr(self.lib, f"tclb_{model}_adjoint")
         self._adj.argtypes = [ctypes.POINTER(Launch)]
@@ -122,15 +124,22 @@ class AdLib:
             raise KernelError(f"{self.model}[ad] stage {L.stage} failed: code {r}")
 
 
-def load_ad(model: str) -> AdLib:
+def load_ad(model: str, gpu: bool = False) -> AdLib:
     from .. import build as B
-    key = (model, "ad", "")
+    kind = "adhip" if gpu else "ad"
+    key = (model, kind, "")
     with _lock:
         if key in _libs:
             return _libs[key]
-        path = B.lib_path(model, "ad")
-        B.build_model(model, kinds=("ad",))
-        lib = AdLib(model, path)
+        path = B.lib_path(model, kind)
+        stale = B.stale_reason(model, kind)
+        if stale is not None:
+            if os.environ.get("TCLB_NO_BUILD"):
+                raise KernelError(f"adjoint library for model '{model}' [{kind}] is not usable ({stale}): {path}")
+            B.build_model(model, kinds=(kind,))
+        if not os.path.exists(path):
+            raise KernelError(f"adjoint library for model '{model}' [{kind}] not built: {path}")
+        lib = AdLib(model, path, kind)
         _libs[key] = lib
         return lib
 

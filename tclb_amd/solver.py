@@ -26,6 +26,7 @@ from .utils.units import UnitEnv, UnitVal
 ITER_NORM = 0x00
 ITER_GLOBS = 0x01
 ITER_LASTGLOB = 0x02
+ITER_OPT = 0x10          # combined primal + steady adjoint + descent (reference ITER_OPT)
 ITERATION_STOP = 1
 
 
@@ -131,12 +132,44 @@ class Solver:
         """one Solve segment (reference Lattice::Iterate with iter_type)"""
         lat = self.lattice
         glob = bool(self.iter_type & (ITER_LASTGLOB | ITER_GLOBS))
+        if self.iter_type & ITER_OPT:
+            for k in range(steps):
+                lat.iterate(1, glob_last=glob and k == steps - 1, action=action or "Iteration")
+                self._opt_iteration(action or "Iteration")
+            self.iter += steps
+            self._speed_meter(steps)
+            return
         if action is None:
             lat.iterate(steps, glob_last=glob)
         else:
             lat.iterate(steps, glob_last=glob, action=action)
         self.iter += steps
         self._speed_meter(steps)
+
+    def _opt_iteration(self, action: str):
+        """the Optimize part of one ITER_OPT iteration (reference Lattice::<Action>_Opt,
+        src/Lattice.cu.Rt:624-636 and the Opt() node function, src/cuda.cu.Rt:241-253):
+        one steady-adjoint step at the current primal state, then on DesignSpace nodes
+        every parameter density moves by Descent x its adjoint, clamped to [0, 1]"""
+        lat = self.lattice
+        ad = self.opt_adjoint
+        self.opt_state = ad.steady_step(self.opt_state, action)
+        descent = lat.get_setting("Descent")
+        pf = ad.param_fields()
+        if not pf or descent == 0.0:
+            return
+        m = self.model
+        mask = m.group_masks.get("DESIGNSPACE")
+        nx, ny, nz = lat.shape
+        sl = (slice(lat.gz, lat.gz + nz), slice(lat.gy, lat.gy + ny), slice(0, nx))
+        fl = lat.flags[sl].to(torch.int64) & 0xFFFFFFFF
+        ds = m.node_type("DesignSpace")
+        sel = ((fl & mask) == ds.value) if (mask and ds is not None) else torch.ones_like(fl, dtype=torch.bool)
+        cur = lat.snaps[lat.cur]
+        for i in pf:
+            p = cur[i][sl]
+            upd = (p + self.opt_state[i][sl] * descent).clamp_(0.0, 1.0)
+            p.copy_(torch.where(sel, upd, p))
 
     def _speed_meter(self, steps: int):
         """reference MainCallback (src/main.cpp:68-157): MLBUps / GB/s"""

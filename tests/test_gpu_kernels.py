@@ -104,13 +104,13 @@ def test_hip_sampler_matches_quantity():
     from tclb_amd.sampler import Sampler
     lat = _mk((64, 16, 8), torch.device("cuda", 0))
     lat.init()
-    smp = Sampler(lat, [(3, 4, 2), (63, 15, 7)], ["Rho", "U"], rows=4)
+    smp = Sampler(lat, [(3, 4, 2), (63, 15, 7)], ["P", "U"], rows=4)
     lat.samplers.append(smp)
     lat.iterate(4)                                   # native loop records 4 rows
     rows = smp.flush()
     assert len(rows) == 8
     u = lat.quantity("U").cpu().numpy()
-    rho = lat.quantity("Rho").cpu().numpy()
+    rho = lat.quantity("P").cpu().numpy()
     for it, i, (x, y, z), v in rows[-2:]:
         assert it == 4
         np.testing.assert_allclose(v, [rho[0, z, y, x], *u[:, z, y, x]], rtol=1e-13)
