@@ -116,7 +116,6 @@ def _cmd(kind: str, src: str, out: str, gen_dir: str, variant: str = "") -> List
             "-Wno-unused-variable", *incs, src, "-o", out]
 
 
-_PY_STAMP: Optional[str] = None
 _PKG = os.path.dirname(os.path.abspath(__file__))
 
 
@@ -131,17 +130,67 @@ def _rel_hash(paths: Iterable[str], extra: str = "") -> str:
     return h.hexdigest()
 
 
-def _python_stamp() -> str:
-    """hash of the model definitions and the emitter (everything a generated header
-    depends on besides csrc): any edit there may change a model's code"""
-    global _PY_STAMP
-    if _PY_STAMP is None:
-        files = []
-        for sub in ("models", "emit"):
-            for d, _, fs in os.walk(os.path.join(_PKG, sub)):
-                files += [os.path.join(d, f) for f in fs if f.endswith(".py")]
-        _PY_STAMP = _rel_hash(files)
-    return _PY_STAMP
+_STAMP_CACHE: Dict[str, str] = {}
+
+
+def _module_file(mod: str, pkg: str) -> Optional[str]:
+    """file of a (possibly relative) module name imported from package `pkg`"""
+    if mod.startswith("."):
+        lvl = len(mod) - len(mod.lstrip("."))
+        parts = pkg.split(".")[:len(pkg.split(".")) - (lvl - 1)]
+        mod = ".".join(parts + ([mod.lstrip(".")] if mod.lstrip(".") else []))
+    if not mod.startswith("tclb_amd."):
+        return None
+    base = os.path.join(os.path.dirname(_PKG), *mod.split("."))
+    for cand in (base + ".py", os.path.join(base, "__init__.py")):
+        if os.path.exists(cand):
+            return cand
+    return None
+
+
+def _import_closure(path: str, pkg: str, seen: set):
+    """the package-local Python files a model module imports, transitively"""
+    import re
+    if path in seen:
+        return
+    seen.add(path)
+    with open(path) as f:
+        src = f.read()
+    for m in re.finditer(r"^\s*from\s+(\.+[\w.]*|tclb_amd[\w.]*)\s+import\s+([\w, ()]+)", src, re.M):
+        mod = m.group(1)
+        fp = _module_file(mod, pkg)
+        names = [n.strip() for n in m.group(2).strip("() ").split(",") if n.strip()]
+        if fp is None or fp.endswith("__init__.py"):
+            # "from .. import x": x may be a submodule
+            for n in names:
+                sub = _module_file(mod + ("." if not mod.endswith(".") else "") + n, pkg)
+                if sub:
+                    sp = ".".join(sub[len(os.path.dirname(_PKG)) + 1:-3].split(os.sep)[:-1])
+                    _import_closure(sub, sp, seen)
+        if fp:
+            sp = ".".join(fp[len(os.path.dirname(_PKG)) + 1:-3].split(os.sep)[:-1])
+            _import_closure(fp, sp, seen)
+
+
+def _python_stamp(name: str) -> str:
+    """hash of what a model's generated header depends on besides csrc: the emitter, the
+    DSL, the model's module and the package modules it imports, and the registry entry
+    (module, builder, options) — an edit elsewhere in models/ leaves the stamp alone"""
+    if name not in _STAMP_CACHE:
+        files = [os.path.join(d, f) for d, _, fs in os.walk(os.path.join(_PKG, "emit")) for f in fs
+                 if f.endswith(".py")]
+        files += [os.path.join(_PKG, "models", "dsl.py"), os.path.join(_PKG, "models", "options.py")]
+        entry = registry._MODELS.get(name) or registry._resolve(name)
+        seen: set = set()
+        if entry is not None:
+            mod = entry[0]
+            fp = _module_file(mod, "tclb_amd.models")
+            if fp:
+                _import_closure(fp, ".".join(fp[len(os.path.dirname(_PKG)) + 1:-3].split(os.sep)[:-1]), seen)
+        files = sorted(set(files) | seen)
+        key = repr((entry[0], entry[1], sorted(entry[2].items()))) if entry else name
+        _STAMP_CACHE[name] = _rel_hash(files, key)
+    return _STAMP_CACHE[name]
 
 
 def source_stamp(name: str, kind: str, variant: str = "") -> str:
@@ -153,7 +202,7 @@ def source_stamp(name: str, kind: str, variant: str = "") -> str:
     v = variant if kind == "hip" else ""
     cmd = _cmd(kind, os.path.join(gdir, "kernels_" + kind), lib_path(name, kind, v), gdir, v)
     deps = _deps_no_gen(model.dynamics) + (_ad_hip_deps() if kind == "adhip" else [])
-    return _rel_hash(deps, " ".join(cmd) + _python_stamp())
+    return _rel_hash(deps, " ".join(cmd) + _python_stamp(name))
 
 
 def _ad_hip_deps() -> List[str]:

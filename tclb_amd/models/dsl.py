@@ -18,11 +18,19 @@ action (src/conf.R:512-586).
 """
 from __future__ import annotations
 
+import os
+
 import math
 import re
 from dataclasses import dataclass, field
 from typing import Callable, Dict, List, Optional, Sequence, Tuple
 
+
+
+# models built with ADJOINT=1 in the reference (their conf.mk): they carry the Descent /
+# GradientSmooth settings of the optimisation loop
+ADJOINT_MODELS = {"d2q9_adj", "d2q9_optimalMixing", "d2q9_heat_adj", "d2q9_kuper_adj", "d3q19_heat_adj", "d3q19_adj",
+                  "d2q9_plate", "sw", "d3q19_heat_adj_art", "d3q19_heat_adj_prop", "d2q9_diff"}
 
 @dataclass
 class Field:
@@ -306,8 +314,12 @@ class Model:
             self.add_setting(f"{g.name}InObj", default=0.0, zonal=True,
                              comment=f"Weight of [{g.comment or g.name}] in objective", preload=False)
         self.add_setting("Threshold", default=0.5, comment="Parameters threshold")
-        if self.setting("Descent") is None:   # reference src/conf.R:735 (ITER_OPT step)
-            self.add_setting("Descent", default=0.0, comment="Optimization Descent")
+        if os.path.basename(self.reference or self.name) in ADJOINT_MODELS:
+            # reference src/conf.R:725-738 (ADJOINT=1 models only)
+            if self.setting("Descent") is None:
+                self.add_setting("Descent", default=0.0, comment="Optimization Descent")
+            if self.setting("GradientSmooth") is None:
+                self.add_setting("GradientSmooth", default=0.0, comment="Gradient smoothing in OptSolve")
         autosym = int(self.options.get("autosym", 0) or 0)
         if autosym:   # automatic symmetry node types (src/conf.R:440-457)
             nm = "Symmetry" if autosym == 1 else "SymmetryEdge"

@@ -301,5 +301,7 @@ for _v in ("d3q27_pf_velocity_thermo", "d3q27_pf_velocity_thermo_planarBenchmark
            "auto_WMRT", "auto_FMT_HiOrd", "auto_d3q19_TRT_autosym", "wave2D_autosym",
            "d3q27q27_cm_cht_OutFlowNeumann_AVG_IBB", "d3q27q7_cm_cht_OutFlowNeumann_AVG_IBB",
            "d2q9q9_cm_cht_OutFlowNeumann_AVG_IBB", "d3q27_cumulant_AVG", "d3q27_cumulant_IB_SMAG",
-           "d3q27_PSM_SEP_singlekernel"):
+           "d3q27_PSM_SEP_singlekernel", "d3q27_pf_velocity_geometric", "d3q27_pf_velocity_staircaseimp",
+           "d3q27_pf_velocity_geometric_staircaseimp_isograd_tprec", "d3q27_tePSM_per_NEBB", "d3q27_tePSM_per_SUP",
+           "d3q27_tePSM_per_NEBB_Isothermal"):
     register_variant(_v)

@@ -154,7 +154,7 @@ class Solver:
         lat = self.lattice
         ad = self.opt_adjoint
         self.opt_state = ad.steady_step(self.opt_state, action)
-        descent = lat.get_setting("Descent")
+        descent = lat.get_setting("Descent") if self.model.setting("Descent") is not None else 0.0
         pf = ad.param_fields()
         if not pf or descent == 0.0:
             return

@@ -54,6 +54,7 @@ CASE_SETTINGS = {
                                  "CenterX": 12.0, "CenterY": 6.0, "CenterZ": 5.0, "BubbleType": -1.0,
                                  "T_init": 1.0, "dT": 0.05, "sigma_T": -1e-4, "k_h": 0.05, "k_l": 0.02,
                                  "cp_h": 1.0, "cp_l": 1.0},
+    "d3q27_tePSM_per": {"omegaF": 1.0, "FluidConductivity": 0.2, "SolidConductivity": 0.5},
     "d3q27_pf_velocity": {"Density_h": 1.0, "Density_l": 0.1, "sigma": 1e-3, "Viscosity_l": 0.05,
                           "Viscosity_h": 0.05, "M": 0.05, "PhaseField": 1.0, "Radius": 4.0,
                           "CenterX": 12.0, "CenterY": 6.0, "CenterZ": 5.0, "BubbleType": -1.0},

@@ -81,6 +81,13 @@ def main():
             rec["status"] = "no model in header"
             print(json.dumps(rec), flush=True)
             continue
+        with open(case, errors="replace") as f:
+            text = f.read()
+        if re.search(r"<\s*(RunR|RunPython)\b", text):
+            # cases embedding R/Python code: the code in the case file is not executed here
+            rec["status"] = "skipped: embedded RunR/RunPython code"
+            print(json.dumps(rec), flush=True)
+            continue
         out = os.path.join(a.out, os.path.splitext(os.path.basename(case))[0])
         os.makedirs(out, exist_ok=True)
         tmp = capped_case(case, a.iters, out)
