@@ -56,6 +56,7 @@ def main():
     ap.add_argument("--model", default="d3q27")
     ap.add_argument("--precision", default="double", choices=list(PRECISIONS))
     ap.add_argument("--weak", action="store_true", help="size^3 per GPU (z-extent x N)")
+    ap.add_argument("--shape", default=None, help="explicit global lattice nx,ny,nz (overrides --size)")
     ap.add_argument("--block", default="0,0")
     ap.add_argument("--no-overlap", action="store_true")
     ap.add_argument("--cpu", action="store_true")
@@ -77,6 +78,8 @@ def main():
         device = torch.device("cpu")
     n = a.size
     shape = (n, n, n * world) if a.weak else (n, n, n)
+    if a.shape:
+        shape = tuple(int(v) for v in a.shape.split(","))
     bx, by = (int(v) for v in a.block.split(","))
     lat = Lattice(a.model, shape, device=device, precision=a.precision, comm=comm, block=(bx, by),
                   overlap=None if not a.no_overlap else False)

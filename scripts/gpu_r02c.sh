@@ -19,9 +19,20 @@ prof) step "rocprof mixed-shift" 400 $O/prof_mixed_shift.log rocprofv3 --kernel-
 counters)
   step "counters d3q27 mixed-shift" 500 $O/counters_d3q27_ms.log python tools/counters.py --tag d3q27_512_mixed_shift --nodes 134217728 --outdir $O/counters -- python3 $R/bench.py --steps 5 --warmup 1 --precision mixed-shift
   step "counters pf384" 500 $O/counters_pf384.log python tools/counters.py --tag pf384_fp64 --nodes 56623104 --outdir $O/counters -- python3 $R/tools/bench_configs.py --configs pf384 --steps 5 --warmup 1 ;;
+pfcounters) step "counters pf384 mixed-shift" 500 $O/counters_pf384_ms.log python tools/counters.py --tag pf384_mixed_shift --nodes 56623104 --outdir $O/counters -- python3 $R/tools/bench_configs.py --configs pf384 --steps 5 --warmup 1 --precision mixed-shift ;;
+modelcounters)
+  step "counters stencil models" 600 $O/counters_models.log python tools/counters.py --tag models_16M --nodes 16777216 --outdir $O/counters -- python3 $R/tools/perf_models.py --models d3q27_PSM_NEBB,d2q9_ShanChen,d2q9_kuper --steps 5
+  step "counters part256" 500 $O/counters_part256.log python tools/counters.py --tag part256_fp64 --nodes 16777216 --outdir $O/counters -- python3 $R/tools/bench_configs.py --configs part256 --steps 5 --warmup 1 ;;
 adjoint)
   step "gpu adjoint tests" 600 $O/pytest_gpu_adjoint.log python -u -m pytest tests/test_gpu_adjoint.py -v -m gpu --timeout 300 --timeout-method thread
-  step "adjoint bench 64" 300 $O/bench_adjoint_64.json python tools/bench_adjoint.py --size 64 --steps 10
-  step "adjoint bench 128" 400 $O/bench_adjoint_128.json python tools/bench_adjoint.py --size 128 --steps 10 ;;
+  step "adjoint bench 64" 300 $O/bench_adjoint_64.json python tools/bench_adjoint.py --size 64 --steps 40
+  step "adjoint bench 128" 400 $O/bench_adjoint_128.json python tools/bench_adjoint.py --size 128 --steps 80 ;;
+dist)
+  step "slab 512x512x64 plain" 300 $O/dist_plain.json python bench.py --shape 512,512,64 --steps 200 --warmup 20
+  step "slab loopback overlap" 300 $O/dist_loop_overlap.json python bench.py --shape 512,512,64 --steps 200 --warmup 20 --loopback-dist
+  step "slab loopback no-overlap" 300 $O/dist_loop_nooverlap.json python bench.py --shape 512,512,64 --steps 200 --warmup 20 --loopback-dist --no-overlap
+  step "slab loopback overlap, pack kernels" 300 $O/dist_loop_overlap_pack.json env TCLB_HALO_MIRROR=0 python bench.py --shape 512,512,64 --steps 200 --warmup 20 --loopback-dist
+  step "rocprof loopback overlap" 400 $O/prof_loop.log rocprofv3 --kernel-trace --stats -d $O/prof_loop -o run --output-format csv -- python3 $R/bench.py --shape 512,512,64 --steps 20 --warmup 5 --loopback-dist ;;
+pfms) step "pf384 storage modes" 600 $O/configs_pf_modes.log bash -c 'for p in double mixed-shift; do python tools/bench_configs.py --configs pf384,cavity --precision $p; done' ;;
 configs) step "configs" 400 $O/configs_r02c.log python tools/bench_configs.py ;;
 esac; done

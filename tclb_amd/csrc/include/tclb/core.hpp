@@ -21,6 +21,7 @@
 #endif
 
 #define TCLB_UNROLL _Pragma("unroll")
+#define TCLB_MIRROR_FIELDS 128   // halo-mirror slot table size (Launch.mslot); models have <= 109 fields
 
 namespace tclb {
 
@@ -68,7 +69,23 @@ struct Launch {
   double time_shift;       // synthetic-turbulence time wave number (Lattice.set_turbulence)
   int storage_shift;       // 1: reduced-precision storage keeps f - shift(field) (see below)
   int reserved2;
+  // Halo mirror (border launches of the overlapped slab step, tclb_amd/lattice.py): every
+  // stored field fi with mslot[fi] >= 0 is also written to
+  // mbase[mslot[fi] * mfs + x + msy * (y + moy) + msz * (z + moz)] — the packed send
+  // buffer of the neighbour exchange, or the wrapped ghost planes of this snapshot —
+  // so no separate pack kernel reads the border planes back.  mbase = null: off.
+  void* mbase;
+  long long mfs, msy, msz;
+  int moy, moz;
+  signed char mslot[TCLB_MIRROR_FIELDS];
 };
+
+template <class S>
+TCLB_FN void mirror_store(const Launch& L, int fi, int x, int y, int z, S v) {
+  const int s = L.mslot[fi];
+  if (s >= 0)
+    ((S*)L.mbase)[(long long)s * L.mfs + x + L.msy * (long long)(y + L.moy) + L.msz * (long long)(z + L.moz)] = v;
+}
 
 // Reduced-precision storage (reference --with-storage=float|half[-shift],
 // src/configure.ac:213-233, src/LatticeAccess.inc.cpp.Rt:14-35).  A density is stored as

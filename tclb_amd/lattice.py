@@ -17,6 +17,7 @@ src/Lattice.cu.Rt).  Differences by design:
 """
 from __future__ import annotations
 
+import ctypes
 import math
 import os
 from typing import Dict, List, Optional, Sequence, Tuple
@@ -140,6 +141,9 @@ class Lattice:
         self.iter = 0
         self.block = block
         self.overlap = (self.comm.distributed if overlap is None else overlap) and ax != 3
+        # overlapped steps pack their outgoing halo inside the border kernels (Launch.mbase);
+        # TCLB_HALO_MIRROR=0 keeps the separate pack kernels (A/B)
+        self.halo_mirror = os.environ.get("TCLB_HALO_MIRROR", "1") != "0"
         kind = "hip" if self.is_gpu else "cpu"
         self.lib = abi.load(m.name, kind, variant=variant)
         # halo field sets per split axis: fields read from below (stencil min < 0) /
@@ -231,20 +235,30 @@ class Lattice:
         axis = self.slab.axis if axis is None else axis
         return buf[:, a:b] if axis == 2 else buf[:, :, a:b]
 
+    def _field_index_t(self, fields: List[int]) -> torch.Tensor:
+        key = tuple(fields)
+        t = self._halo_bufs.get(key)
+        if t is None:
+            t = self._halo_bufs[key] = torch.tensor(fields, dtype=torch.long, device=self.device)
+        return t
+
     def _pack(self, buf: torch.Tensor, fields: List[int], a: int, b: int, axis: Optional[int] = None) -> torch.Tensor:
+        """the halo planes of `fields` as one contiguous message: one strided copy for a
+        contiguous run of fields, else one gather kernel (index_select)"""
         planes = self._axis_planes(buf, a, b, axis)
         runs = _runs(fields)
         if len(runs) == 1:
             return planes[runs[0][0]:runs[0][1]].contiguous()
-        return torch.cat([planes[r0:r1] for r0, r1 in runs], 0).contiguous()
+        return planes.index_select(0, self._field_index_t(fields))
 
     def _unpack(self, buf: torch.Tensor, fields: List[int], a: int, b: int, data: torch.Tensor,
                 axis: Optional[int] = None):
         planes = self._axis_planes(buf, a, b, axis)
-        k = 0
-        for r0, r1 in _runs(fields):
-            planes[r0:r1].copy_(data[k:k + (r1 - r0)])
-            k += r1 - r0
+        runs = _runs(fields)
+        if len(runs) == 1:
+            planes[runs[0][0]:runs[0][1]].copy_(data)
+        else:
+            planes.index_copy_(0, self._field_index_t(fields), data)      # one scatter kernel
 
     def _halo_start(self, buf: torch.Tensor, fields: Optional[Sequence[int]] = None):
         if self.g == 0:
@@ -293,6 +307,74 @@ class Lattice:
             self._unpack(buf, hi, n + g, n + 2 * g, ra, axis)
         if trace.ENABLED:
             trace.pop()
+
+    def _mirror_buffer(self, fields: List[int], axis: int) -> torch.Tensor:
+        """persistent packed halo buffer [len(fields)][g planes] of one side, laid out as
+        _pack's output (zeroed once, so the x pitch padding stays finite)"""
+        key = ("mirror", axis, tuple(fields))
+        t = self._halo_bufs.get(key)
+        if t is None:
+            g = self.gz if axis == 2 else self.gy
+            shape = (len(fields), g, self.NY, self.px) if axis == 2 else (len(fields), self.NZ, g, self.px)
+            t = self._halo_bufs[key] = torch.zeros(shape, dtype=self.sdtype, device=self.device)
+        return t
+
+    def _launch_mirrored(self, stage: int, src, dst, glob: bool, rng: Tuple[int, int], fields: List[int],
+                         target: torch.Tensor, axis: int):
+        """launch over border planes rng whose stores of `fields` also land in the packed
+        buffer `target` (Launch.mbase, core.hpp mirror_store): the border kernel packs the
+        outgoing halo itself"""
+        L = self._L
+        key = ("slots", tuple(fields))
+        table = self._halo_bufs.get(key)
+        if table is None:
+            vals = [-1] * abi.MIRROR_FIELDS
+            for k, f in enumerate(fields):
+                vals[f] = k
+            table = self._halo_bufs[key] = (ctypes.c_byte * abi.MIRROR_FIELDS)(*vals)
+        L.mslot = table
+        L.mbase = target.data_ptr()
+        L.mfs = target.stride(0)
+        if axis == 2:
+            L.msy, L.msz, L.moy, L.moz = self.px, self.NY * self.px, self.gy, -rng[0]
+        else:
+            L.msy, L.msz, L.moy, L.moz = self.px, target.shape[2] * self.px, -rng[0], self.gz
+        try:
+            self._launch_stage(stage, src, dst, glob, rng)
+        finally:
+            L.mbase = None
+
+    def _border_mirrored(self, stage: int, src, dst, glob: bool, fields: List[int]):
+        """overlapped slab step, border part: the two border launches write their halo
+        planes straight into the send buffers (no pack kernels), then the exchange starts.
+        Reference: RunBorder + MPIStream_A (src/Lattice.cu.Rt:466-533), which packs the
+        margin blocks on the device in separate copy kernels."""
+        axis = self.slab.axis
+        g = self.gz if axis == 2 else self.gy
+        n = self.shape[2] if axis == 2 else self.shape[1]
+        lo_set, hi_set = self.halo_sets[axis]
+        fs = set(fields)
+        lo = [i for i in lo_set if i in fs]        # read from below: my top planes go up
+        hi = [i for i in hi_set if i in fs]        # read from above: my bottom planes go down
+        send_down = self._mirror_buffer(hi, axis) if hi else None
+        send_up = self._mirror_buffer(lo, axis) if lo else None
+        if hi:
+            self._launch_mirrored(stage, src, dst, glob, (0, g), hi, send_down, axis)
+        else:
+            self._launch_stage(stage, src, dst, glob, (0, g))
+        if lo:
+            self._launch_mirrored(stage, src, dst, glob, (n - g, n), lo, send_up, axis)
+        else:
+            self._launch_stage(stage, src, dst, glob, (n - g, n))
+        if trace.ENABLED:
+            trace.push("halo")
+        if isinstance(self.comm, LoopbackComm):
+            # this rank is its own neighbour: the send buffers are the received halos
+            return (None, dst, lo, hi, send_up, send_down, send_up, send_down, axis)
+        recv_below = torch.empty_like(send_up) if lo else None
+        recv_above = torch.empty_like(send_down) if hi else None
+        h = self.comm.start_halo(send_up, send_down, recv_below, recv_above)
+        return (h, dst, lo, hi, recv_below, recv_above, send_up, send_down, axis)
 
     def exchange(self, buf: Optional[torch.Tensor] = None, fields=None):
         buf = self.snaps[self.cur] if buf is None else buf
@@ -347,9 +429,12 @@ class Lattice:
                         dst[r0:r1].copy_(scratch[r0:r1])
                     self._halo_finish(self._halo_start(dst, fields))
             elif self.overlap and n > 2 * g:
-                self._launch_stage(si, inp, dst, glob, (0, g))
-                self._launch_stage(si, inp, dst, glob, (n - g, n))
-                hs = self._halo_start(dst, fields)
+                if self.halo_mirror:
+                    hs = self._border_mirrored(si, inp, dst, glob, fields)
+                else:
+                    self._launch_stage(si, inp, dst, glob, (0, g))
+                    self._launch_stage(si, inp, dst, glob, (n - g, n))
+                    hs = self._halo_start(dst, fields)
                 self._launch_stage(si, inp, dst, glob, (g, n - g))
                 self._halo_finish(hs)
             else:

@@ -16,6 +16,8 @@ from typing import Dict, Optional
 
 import torch  # noqa: F401  (must be imported before loading HIP libraries)
 
+MIRROR_FIELDS = 128     # core.hpp TCLB_MIRROR_FIELDS
+
 
 class Launch(ctypes.Structure):
     _fields_ = [
@@ -53,6 +55,14 @@ class Launch(ctypes.Structure):
         ("time_shift", ctypes.c_double),
         ("storage_shift", ctypes.c_int),
         ("reserved2", ctypes.c_int),
+        # halo mirror of the border launches (core.hpp mirror_store)
+        ("mbase", ctypes.c_void_p),
+        ("mfs", ctypes.c_longlong),
+        ("msy", ctypes.c_longlong),
+        ("msz", ctypes.c_longlong),
+        ("moy", ctypes.c_int),
+        ("moz", ctypes.c_int),
+        ("mslot", ctypes.c_byte * MIRROR_FIELDS),
     ]
 
 

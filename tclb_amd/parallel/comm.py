@@ -165,7 +165,17 @@ def init_distributed_from_env(device: str = "auto") -> Optional[Comm]:
     os.environ.setdefault("MASTER_PORT", "29511")
     use_gpu = device == "cuda" or (device == "auto" and torch.cuda.is_available())
     backend = "nccl" if use_gpu else "gloo"
+    kw = {}
     if use_gpu:
         torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
-    dist.init_process_group(backend=backend)
+        # halo P2P runs on RCCL's internal stream while the interior kernel fills the CUs:
+        # a high-priority stream lets its work-groups dispatch as soon as CUs free up
+        if os.environ.get("TCLB_RCCL_HIGH_PRIORITY", "1") != "0":
+            try:
+                opts = dist.ProcessGroupNCCL.Options()
+                opts.is_high_priority_stream = True
+                kw["pg_options"] = opts
+            except (AttributeError, RuntimeError):
+                pass
+    dist.init_process_group(backend=backend, **kw)
     return make_comm()

@@ -9,3 +9,11 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (HIP kernels on cuda:0)")
     config.addinivalue_line("markers", "slow: long-running test")
+
+
+@pytest.fixture(autouse=True)
+def _restore_cwd():
+    """tests that chdir into tmp_path must not leave later tests in a deleted directory"""
+    cwd = os.getcwd()
+    yield
+    os.chdir(cwd)

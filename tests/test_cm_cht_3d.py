@@ -170,15 +170,14 @@ CHT_XML = """<?xml version="1.0"?>
 </CLBConfig>"""
 
 
-def test_cht_xml_case(tmp_path):
+def test_cht_xml_case(tmp_path, monkeypatch):
     """XML case (Geometry zones, zonal Param, Solve, VTK, Log) on d3q27q7_cm_cht: the heated
     patch raises T, T stays within [9.9, 11], and the HeatSource global is logged"""
-    import os
     import xml.etree.ElementTree as ET
     from tclb_amd import handlers  # noqa: F401
     from tclb_amd.io.vtk import read_vti
     from tclb_amd.solver import Solver
-    os.chdir(tmp_path)
+    monkeypatch.chdir(tmp_path)
     s = Solver("d3q27q7_cm_cht", ET.fromstring(CHT_XML), conffile=str(tmp_path / "case.xml"), device="cpu")
     s.run()
     assert s.iter == 100

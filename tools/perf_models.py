@@ -41,7 +41,7 @@ def main():
             lat.iterate(a.steps, glob_last=False)
             torch.cuda.synchronize()
             dt = (time.perf_counter() - t) / a.steps
-            es = 8 if a.precision == "double" else 4
+            es = lat.snaps[0].element_size()
             nodes = shape[0] * shape[1] * shape[2]
             bpn = 2 * lat.nf * es + lat.flags.element_size()
             print(json.dumps({"model": name, "variant": variant, "round": rnd, "shape": shape, "fields": lat.nf, "stages": len(m.stages),
