@@ -23,6 +23,11 @@ pfcounters) step "counters pf384 mixed-shift" 500 $O/counters_pf384_ms.log pytho
 modelcounters)
   step "counters stencil models" 600 $O/counters_models.log python tools/counters.py --tag models_16M --nodes 16777216 --outdir $O/counters -- python3 $R/tools/perf_models.py --models d3q27_PSM_NEBB,d2q9_ShanChen,d2q9_kuper --steps 5
   step "counters part256" 500 $O/counters_part256.log python tools/counters.py --tag part256_fp64 --nodes 16777216 --outdir $O/counters -- python3 $R/tools/bench_configs.py --configs part256 --steps 5 --warmup 1 ;;
+ldsab)
+  step "lds a/b 384" 300 $O/lds_ab_384.log python tools/lds_ab.py --n 384 --reps 20
+  step "lds a/b 512" 300 $O/lds_ab_512.log python tools/lds_ab.py --n 512 --reps 10
+  step "counters lds a/b" 400 $O/counters_lds.log python tools/counters.py --tag lds_ab_384 --nodes 56623104 --outdir $O/counters -- python3 $R/tools/lds_ab.py --n 384 --reps 3 --rounds 1 ;;
+nwab) step "narrow-storage occupancy A/B" 900 $O/nw_ab.log python tools/perf_models.py --models d3q27_pf_velocity,d3q27 --n3 384 --steps 10 --precision mixed-shift --variants ",nw3,nw4" --rounds 2 ;;
 adjoint)
   step "gpu adjoint tests" 600 $O/pytest_gpu_adjoint.log python -u -m pytest tests/test_gpu_adjoint.py -v -m gpu --timeout 300 --timeout-method thread
   step "adjoint bench 64" 300 $O/bench_adjoint_64.json python tools/bench_adjoint.py --size 64 --steps 40

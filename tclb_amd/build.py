@@ -36,6 +36,9 @@ VARIANTS = {
     "ntld": ["-DTCLB_NT_LOAD=1"],
     "noxs": ["-DTCLB_DEBUG_NO_XSHIFT", "-DTCLB_NT_STORE=1"],   # diagnostic: aligned-x ceiling
     "xcd": ["-DTCLB_NT_STORE=1", "-DTCLB_XCD_REMAP=1"],        # XCD-contiguous block->tile map
+    # occupancy floor for the fp32/fp16-storage kernels (executor_hip.hpp k_stage_narrow)
+    "nw3": ["-DTCLB_NT_STORE=1", "-DTCLB_NARROW_WAVES=3"],
+    "nw4": ["-DTCLB_NT_STORE=1", "-DTCLB_NARROW_WAVES=4"],
 }
 DEFAULT_VARIANT = os.environ.get("TCLB_VARIANT", "")
 
@@ -263,22 +266,25 @@ def build_model(name: str, kinds=("cpu", "hip"), force: bool = False, verbose: b
         t0 = time.time()
         tmp = f"{target}.{os.getpid()}.{threading.get_ident()}.tmp"
         cmd[-1] = tmp
+        # stamps describe the sources as they were when the compiler read them: an edit
+        # made during the compile leaves the library stale, not falsely fresh
+        src_stamp = source_stamp(name, kind, variant)
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"build of {name} [{kind}] failed:\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr[-20000:]}")
         os.replace(tmp, target)
         with open(stamp, "w") as f:
             f.write(h)
-        _write_src_stamp(name, kind, variant)
+        _write_src_stamp(name, kind, variant, src_stamp)
         if verbose:
             print(f"[tclb build] {name} [{kind}{'/' + v if v else ''}] {time.time() - t0:.1f}s", flush=True)
         out[kind] = target
     return out
 
 
-def _write_src_stamp(name: str, kind: str, variant: str):
+def _write_src_stamp(name: str, kind: str, variant: str, s: Optional[str] = None):
     v = variant if kind == "hip" else ""
-    s = source_stamp(name, kind, variant)
+    s = source_stamp(name, kind, variant) if s is None else s
     p = lib_path(name, kind, v) + ".src"
     if not os.path.exists(p) or open(p).read() != s:
         with open(p, "w") as f:
@@ -337,6 +343,41 @@ def build_tools(force: bool = False, verbose: bool = False) -> Dict[str, str]:
                 f.write(h)
             if verbose:
                 print(f"[tclb build] tool tclb-{name}", flush=True)
+        out[name] = target
+    return out
+
+
+def bench_lib_path(name: str) -> str:
+    return os.path.join(LIB, f"libtclb_{name}.so")
+
+
+def build_bench_libs(force: bool = False, verbose: bool = False) -> Dict[str, str]:
+    """stand-alone HIP micro-benchmarks (csrc/bench/<name>.hip -> _build/lib/libtclb_<name>.so),
+    e.g. the LDS A/B of the 27-point stencil (tools/lds_ab.py)"""
+    bdir = os.path.join(CSRC, "bench")
+    os.makedirs(LIB, exist_ok=True)
+    out = {}
+    if not os.path.exists(HIPCC):
+        return out
+    for fn in sorted(os.listdir(bdir)):
+        if not fn.endswith(".hip"):
+            continue
+        name = fn[:-4]
+        src = os.path.join(bdir, fn)
+        target = bench_lib_path(name)
+        tmp = f"{target}.{os.getpid()}.tmp"
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", src, "-o"]
+        h = _hash_inputs([src], " ".join(cmd))
+        stamp = target + ".hash"
+        if force or not (os.path.exists(target) and os.path.exists(stamp) and open(stamp).read() == h):
+            r = subprocess.run(cmd + [tmp], capture_output=True, text=True)
+            if r.returncode != 0:
+                raise RuntimeError(f"bench lib {name} build failed:\n{r.stderr[-10000:]}")
+            os.replace(tmp, target)
+            with open(stamp, "w") as f:
+                f.write(h)
+            if verbose:
+                print(f"[tclb build] bench lib {name}", flush=True)
         out[name] = target
     return out
 

@@ -87,7 +87,7 @@ __device__ __forceinline__ uint3 tile_id() {
 }
 
 template <class Model, class R, class S, int STG, bool GLOB>
-__global__ void __launch_bounds__(256) k_stage(const Launch L) {
+__device__ __forceinline__ void stage_body(const Launch& L) {
   const uint3 t = tile_id();
   const int x = L.xlo + (int)(t.x * blockDim.x + threadIdx.x);
   const int y = L.ylo + (int)(t.y * blockDim.y + threadIdx.y);
@@ -102,6 +102,23 @@ __global__ void __launch_bounds__(256) k_stage(const Launch L) {
   }
   if constexpr (GLOB) block_globals<NG, Model::NSUMGLOBALS_>(g, L.globals);
 }
+
+template <class Model, class R, class S, int STG, bool GLOB>
+__global__ void __launch_bounds__(256) k_stage(const Launch L) {
+  stage_body<Model, R, S, STG, GLOB>(L);
+}
+
+// Narrow-storage occupancy floor (build variant, -DTCLB_NARROW_WAVES=N): with fp32/fp16
+// storage each load moves half (a quarter) of the bytes, so a register-heavy kernel that
+// keeps HBM busy at 2 waves/SIMD in fp64 needs more waves in flight (Little's law);
+// amdgpu_waves_per_eu caps the VGPRs of the narrow-storage instantiations only.
+#ifdef TCLB_NARROW_WAVES
+template <class Model, class R, class S, int STG, bool GLOB>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TCLB_NARROW_WAVES)))
+k_stage_narrow(const Launch L) {
+  stage_body<Model, R, S, STG, GLOB>(L);
+}
+#endif
 
 template <class Model, class R, class S>
 __global__ void __launch_bounds__(256) k_quantity(const Launch L) {
@@ -150,6 +167,12 @@ inline void launch_shape(const Launch& L, dim3& grid, dim3& block, int sbytes = 
 
 template <class Model, class R, class S, int I, bool G>
 inline bool launch_one(const Launch& L, dim3 grid, dim3 block, hipStream_t s) {
+#ifdef TCLB_NARROW_WAVES
+  if constexpr (sizeof(S) < sizeof(double)) {
+    k_stage_narrow<Model, R, S, I, G><<<grid, block, 0, s>>>(L);
+    return true;
+  }
+#endif
   k_stage<Model, R, S, I, G><<<grid, block, 0, s>>>(L);
   return true;
 }

@@ -11,6 +11,10 @@ Options (reference OPT="OutFlowConvective*OutFlowNeumann*AVG*IBB*SMAG*CHT"):
   CHT  sigma^2 = h_stability_enhancement / (3 cp rho) in the heat equilibria;
   IBB  interpolated (anti-)bounce-back on STL cuts; AVG running averages;
   SMAG Smagorinsky eddy viscosity; OutFlowConvective / OutFlowNeumann east outlets.
+heat_q=27 (d3q27q27_cm_cht): CM_HIGHER_PROB, CM_HIGHER_PROB_M_EQ and the cumulant heat
+collisions normalise by H = sum(h) (k[1]/k[0], cum_raw2cum), as the reference does
+(h100/h000): a node with H = 0 (the default InitTemperature = 0) turns NaN and spreads it
+by streaming.  Initialise a nonzero temperature before using them.
 Reference: models/heat/d3q27q7_cm_cht/{Dynamics.R:1-224, Dynamics.c.Rt:247-1487}.
 """
 import numpy as np
@@ -105,7 +109,9 @@ def build(outflowconvective=False, outflowneumann=False, avg=False, ibb=False, s
         m.add_node_type("CM", "COLLISION")
         m.add_node_type("CM_PROB", "COLLISION")
     else:
-        for n in ("CM_HIGHER", "CM_HIGHER_PROB", "CM_HIGHER_PROB_M_EQ", "Cumulants", "Cumulants_HIGHER", "CM"):
+        # reference registration order (models/heat/d3q27q27_cm_cht/Dynamics.R:114-119):
+        # flag values follow it, so raw NodeType dumps match the reference's
+        for n in ("CM", "CM_HIGHER", "CM_HIGHER_PROB", "CM_HIGHER_PROB_M_EQ", "Cumulants", "Cumulants_HIGHER"):
             m.add_node_type(n, "COLLISION")
     S("CylinderCenterX", default=0, comment="X coord of cylinder with imposed heat flux")
     S("CylinderCenterY", default=0, comment="Y coord of cylinder with imposed heat flux")

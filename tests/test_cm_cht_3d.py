@@ -190,3 +190,47 @@ def test_cht_xml_case(tmp_path, monkeypatch):
     assert t.max() > 10.01
     log = open(tmp_path / "output" / "case_Log_P00_00000000.csv").read().splitlines()
     assert "HeatSource" in log[0]
+
+
+def test_q27_collision_types_in_reference_order():
+    """flag values follow the reference's registration order (models/heat/d3q27q27_cm_cht/
+    Dynamics.R:114-119, BGK at :221), so raw NodeType dumps are interchangeable"""
+    from tclb_amd.models import registry
+    m = registry.get("d3q27q27_cm_cht")
+    names = ["CM", "CM_HIGHER", "CM_HIGHER_PROB", "CM_HIGHER_PROB_M_EQ", "Cumulants", "Cumulants_HIGHER", "BGK"]
+    vals = [m.node_type(n).value for n in names]
+    assert vals == sorted(vals) and len(set(vals)) == len(vals)
+
+
+def test_neumann_flux_q27_increment_moments():
+    """the east Neumann heater adds raw moments m100 = n_x first, m120 = m102 = n_x first s2
+    and m122 = n_x first s2^2 (first = -2 InitHeatFlux h_stability_enhancement, s2 = 1/3,
+    reference ImposeHeatFlux): one step with and without the flux on heater nodes that do
+    not collide, difference of the stored h, raw moments"""
+    def run(flux):
+        lat = Lattice("d3q27q27_cm_cht", (4, 3, 3))
+        m = lat.model
+        zi = lat.zone_index("hot")
+        fl = np.full((lat.NZ, lat.NY, 4), m.node_type("CM_HIGHER").value, dtype=np.uint32)
+        fl[:, :, 0] = m.node_type("HeaterNeumannHeatFluxEast").value | (zi << m.zone_shift)
+        lat.set_flags(fl)
+        lat.set_setting("InitTemperature", 1.0)
+        lat.set_setting("InitHeatFlux", flux, zone="hot")
+        lat.init()
+        lat.iterate(1)
+        dens = [d for d in m.densities if d.field.group == "h"]
+        hi = [m.fields.index(d.field) for d in dens]
+        C = np.array([[d.dx, d.dy, d.dz] for d in dens], dtype=float)
+        return lat, C, lat.fields_interior()[hi][:, :, :, 0].numpy()
+    lat, C, ha = run(0.01)
+    _, _, hb = run(0.0)
+    d = ha - hb
+    hs = lat.svals[lat.gsettings.index("h_stability_enhancement")] if "h_stability_enhancement" in lat.gsettings else 1.0
+    first = -2 * 0.01 * hs
+    s2 = 1 / 3
+    expect = {(1, 0, 0): -first, (1, 2, 0): -first * s2, (1, 0, 2): -first * s2, (1, 2, 2): -first * s2 * s2}
+    for a in range(3):
+        for b in range(3):
+            for c in range(3):
+                mom = np.tensordot(C[:, 0] ** a * C[:, 1] ** b * C[:, 2] ** c, d, 1)
+                np.testing.assert_allclose(mom, expect.get((a, b, c), 0.0), atol=1e-15, err_msg=str((a, b, c)))
