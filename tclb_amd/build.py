@@ -41,6 +41,18 @@ VARIANTS = {
     "nw4": ["-DTCLB_NT_STORE=1", "-DTCLB_NARROW_WAVES=4"],
 }
 DEFAULT_VARIANT = os.environ.get("TCLB_VARIANT", "")
+# CPU executor variants: "ubsan" builds the node code with UndefinedBehaviorSanitizer
+# (host code only; the runtime is a plain shared dependency, no preload needed)
+CPU_VARIANTS = {
+    "ubsan": ["-fsanitize=undefined", "-fno-sanitize-recover=undefined", "-fno-omit-frame-pointer", "-g1"],
+}
+
+
+def _variant_of(kind: str, variant: str) -> str:
+    """the variant a library of this kind is built in ("" for kinds without variants)"""
+    if kind == "hip" or (kind == "cpu" and variant in CPU_VARIANTS):
+        return variant
+    return ""
 
 
 def lib_path(model: str, kind: str, variant: str = "") -> str:
@@ -115,8 +127,9 @@ def _cmd(kind: str, src: str, out: str, gen_dir: str, variant: str = "") -> List
                 "-Wno-unused-result", "-Wno-pass-failed", *VARIANTS[variant], *incs,
                 src, "-o", out]
     opt = "-O2" if kind == "ad" else "-O3"
+    extra = CPU_VARIANTS.get(variant, []) if kind == "cpu" else []
     return [CXX, opt, "-std=c++17", "-fPIC", "-shared", "-fopenmp", "-fno-strict-aliasing",
-            "-Wno-unused-variable", *incs, src, "-o", out]
+            "-Wno-unused-variable", *extra, *incs, src, "-o", out]
 
 
 _PKG = os.path.dirname(os.path.abspath(__file__))
@@ -202,7 +215,7 @@ def source_stamp(name: str, kind: str, variant: str = "") -> str:
     stored next to the library as <lib>.src and checked by ops.abi.load without emitting"""
     model = registry.get(name)
     gdir = os.path.join(BUILD, "gen", name)
-    v = variant if kind == "hip" else ""
+    v = _variant_of(kind, variant)
     cmd = _cmd(kind, os.path.join(gdir, "kernels_" + kind), lib_path(name, kind, v), gdir, v)
     deps = _deps_no_gen(model.dynamics) + (_ad_hip_deps() if kind == "adhip" else [])
     return _rel_hash(deps, " ".join(cmd) + _python_stamp(name))
@@ -230,7 +243,7 @@ def _deps_no_gen(dynamics: Optional[str]) -> List[str]:
 
 def stale_reason(name: str, kind: str, variant: str = "") -> Optional[str]:
     """None when the library exists and was built from the current sources"""
-    v = variant if kind == "hip" else ""
+    v = _variant_of(kind, variant)
     target = lib_path(name, kind, v)
     if not os.path.exists(target):
         return "missing"
@@ -252,7 +265,7 @@ def build_model(name: str, kinds=("cpu", "hip"), force: bool = False, verbose: b
     for kind in kinds:
         if kind in ("hip", "adhip") and not os.path.exists(HIPCC):
             continue
-        v = variant if kind == "hip" else ""
+        v = _variant_of(kind, variant)
         target = lib_path(name, kind, v)
         src = _adhip_source(model, paths["dir"]) if kind == "adhip" else paths[kind]
         cmd = _cmd(kind, src, target, paths["dir"], v)
@@ -283,7 +296,7 @@ def build_model(name: str, kinds=("cpu", "hip"), force: bool = False, verbose: b
 
 
 def _write_src_stamp(name: str, kind: str, variant: str, s: Optional[str] = None):
-    v = variant if kind == "hip" else ""
+    v = _variant_of(kind, variant)
     s = source_stamp(name, kind, variant) if s is None else s
     p = lib_path(name, kind, v) + ".src"
     if not os.path.exists(p) or open(p).read() != s:
