@@ -842,8 +842,14 @@ class SyntheticTurbulenceAction(Action):
 @register("RemoteForceInterface")
 class RemoteForceInterface(Action):
     """reference acRemoteForceInterface (src/Handlers/acRemoteForceInterface.cpp): connects
-    the lattice to a particle integrator.  Supported integrator: SIMPLEPART (built-in,
-    in-process; configuration from the <SimplePart> child as in the reference)."""
+    the lattice to a particle integrator.  integrator="SIMPLEPART" (or BUILTIN): the
+    built-in in-process integrator, configured from the <SimplePart> child as in the
+    reference.  Any other integrator runs as another program and couples over the socket
+    RFI bridge (particles/rfi.py): the lattice listens on ``address`` (default
+    127.0.0.1:0 = any free port) and ``spawn`` (optional) starts the integrator with
+    ``{address}`` replaced, e.g.
+    ``spawn="python tools/rfi_simplepart.py --address {address} --config parts.json"``.
+    The reference launches its integrators MPMD-style (mpirun -np 1 tclb : -np 1 lammps)."""
 
     def init(self):
         super().init()
@@ -851,7 +857,7 @@ class RemoteForceInterface(Action):
         s = self.solver
         integ = (self.node.get("integrator") or "").upper()
         if integ not in ("SIMPLEPART", "BUILTIN"):
-            raise HandlerError(f"RemoteForceInterface integrator '{integ}' not available (use SIMPLEPART)")
+            return self._remote()
         sp = SimplePart()
         u = s.units
         off = [u.alt(s.config_tree.find("Geometry").get("p" + a, "0")) for a in "xyz"]
@@ -887,6 +893,34 @@ class RemoteForceInterface(Action):
         s.lattice.particles = sp
         s.particles = sp
         log.output(f"RemoteForceInterface: {sp.n} particle(s) with built-in SIMPLEPART integrator")
+        return 0
+
+    def _remote(self):
+        import os
+        import shlex
+        import subprocess
+        from ..particles.rfi import RemoteParticles
+        s = self.solver
+        lat = s.lattice
+        u = s.units
+        units = {"m": u.alt("1m"), "s": u.alt("1s"), "kg": u.alt("1kg")}
+        rp = RemoteParticles(self.node.get("address", "127.0.0.1:0"), comm=lat.comm, units=units,
+                             box=list(lat.gshape), timeout=float(self.node.get("timeout", "120")))
+        proc = None
+        cmd = self.node.get("spawn")
+        if cmd and lat.comm.rank == 0:
+            cwd = os.path.dirname(os.path.abspath(s.conffile)) if getattr(s, "conffile", None) else None
+            proc = subprocess.Popen(shlex.split(cmd.replace("{address}", rp.address)), cwd=cwd)
+        log.output(f"RemoteForceInterface: waiting for integrator '{self.node.get('integrator')}' on {rp.address}")
+        rp.accept()
+        lat.particles = rp
+        s.particles = rp
+
+        def stop():
+            rp.close()
+            if proc is not None:
+                proc.wait(timeout=60)
+        s.at_exit = getattr(s, "at_exit", []) + [stop]
         return 0
 
 

@@ -7,5 +7,8 @@ stage (a few KB), the stage kernel (model ``CalcF`` through ``ParticleLoop``)
 accumulates force and moment per particle with wave-reduced atomics, the sums are
 all-reduced across ranks (RCCL/gloo) and the built-in rigid-body integrator
 ("SimplePart") advances the particles.  No MPMD intercommunicator is needed.
+An integrator that runs as another program (a DEM code, tools/rfi_simplepart.py)
+couples through the socket RFI bridge in ``rfi.py``.
 """
-from .system import ParticleSystem, SimplePart  # noqa: F401
+from .system import ParticleSystem, SimplePart, integrate_rigid  # noqa: F401
+from .rfi import IntegratorClient, RemoteParticles  # noqa: F401

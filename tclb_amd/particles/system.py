@@ -89,6 +89,21 @@ class ParticleSystem:
         """advance after the particle stage of one iteration"""
 
 
+def integrate_rigid(x, v, omega, r, m, fixed, force, torque, acc, periodic, period):
+    """one explicit step of free rigid spheres (reference simplepart.cpp), in place; shared
+    by the in-process SimplePart and the remote integrator tools/rfi_simplepart.py"""
+    for i in range(len(r)):
+        if fixed[i]:
+            continue
+        I = 0.4 * m[i] * r[i] ** 2
+        v[i] += force[i] / m[i] + acc
+        x[i] += v[i]
+        omega[i] += torque[i] / I
+        for d in range(3):
+            if periodic[d] and period[d] > 0:
+                x[i, d] %= period[d]
+
+
 class SimplePart(ParticleSystem):
     """Built-in rigid spheres (reference simplepart: explicit integration, optional
     periodicity, constant acceleration, logging)."""
@@ -106,17 +121,8 @@ class SimplePart(ParticleSystem):
 
     def step(self, lat):
         self.iteration += 1
-        for i in range(self.n):
-            if self.fixed[i]:
-                continue
-            m = self.m[i]
-            I = 0.4 * m * self.r[i] ** 2
-            self.v[i] += self.force[i] / m + self.acc
-            self.x[i] += self.v[i]
-            self.omega[i] += self.torque[i] / I
-            for d in range(3):
-                if self.periodic[d] and self.period[d] > 0:
-                    self.x[i, d] %= self.period[d]
+        integrate_rigid(self.x, self.v, self.omega, self.r, self.m, self.fixed, self.force, self.torque, self.acc,
+                        self.periodic, self.period)
         if self.log_path and self.iteration % self.log_every == 0 and lat.comm.rank == 0:
             self._log()
 

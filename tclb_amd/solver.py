@@ -122,10 +122,15 @@ class Solver:
         from .handlers.base import make_handler
         self.read_units()
         self.set_size()
-        root = make_handler(self.config_tree, self)
-        if root is None:
-            raise SolverError("root handler failed")
-        root.finish()
+        try:
+            root = make_handler(self.config_tree, self)
+            if root is None:
+                raise SolverError("root handler failed")
+            root.finish()
+        finally:
+            # end-of-run hooks (e.g. the RFI death protocol towards a remote integrator)
+            for fn in reversed(getattr(self, "at_exit", [])):
+                fn()
         return 0
 
     def iterate(self, steps: int, action: Optional[str] = None):
