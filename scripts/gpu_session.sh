@@ -1,19 +1,19 @@
 #!/bin/bash
-# r02 third GPU session: tests (sampler, reduced storage, scmp/csf fixes), benches of
-# the storage modes, karman compute-only, counters / kernel stats.
-#   scripts/gpu_r02c.sh [tests] [bench] [karman] [prof] [counters] [configs]
+# developer GPU session: every step writes gpurun_out/$TAG/<step>.log
+#   TAG=r02h scripts/gpu_session.sh [tests] [bench] [karman] [prof] [counters] [configs] ...
+# each GPU step has its own timeout; a crash / timeout (rc >= 124) ends the call
 set -o pipefail
-R=${GRAFT_REPO_ROOT:-$(pwd)}; O=$R/gpurun_out; mkdir -p $O; cd $R
+R=${GRAFT_REPO_ROOT:-$(pwd)}; TAG=${TAG:-run}; O=$R/gpurun_out/$TAG; mkdir -p $O; cd $R
 step() { local name=$1 t=$2 log=$3; shift 3; echo "== $name"; timeout -k 10 $t "$@" > $log 2>&1; local rc=$?; tail -4 $log; echo "   rc=$rc"; if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi; return 0; }
 export TMPDIR=/tmp
 for W in "$@"; do case $W in
-newtests) step "new gpu tests" 400 $O/pytest_gpu_r02c_new.log python -u -m pytest tests/test_gpu_oracles.py tests/test_gpu_kernels.py -v -m gpu --timeout 120 --timeout-method thread ;;
-tests) step "gpu tests" 900 $O/pytest_gpu_r02c.log python -u -m pytest tests -v -m gpu --timeout 120 --timeout-method thread ;;
+newtests) step "new gpu tests" 400 $O/pytest_gpu_new.log python -u -m pytest tests/test_gpu_oracles.py tests/test_gpu_kernels.py -v -m gpu --timeout 120 --timeout-method thread ;;
+tests) step "gpu tests" 900 $O/pytest_gpu.log python -u -m pytest tests -v -m gpu --timeout 120 --timeout-method thread ;;
 bench)
-  step "bench fp64" 300 $O/bench_r02c_fp64.json python bench.py
-  step "bench mixed-shift" 300 $O/bench_r02c_mixed_shift.json python bench.py --precision mixed-shift
-  step "bench mixed" 300 $O/bench_r02c_mixed.json python bench.py --precision mixed
-  step "bench half-shift" 300 $O/bench_r02c_half_shift.json python bench.py --precision half-shift ;;
+  step "bench fp64" 300 $O/bench_fp64.json python bench.py
+  step "bench mixed-shift" 300 $O/bench_mixed_shift.json python bench.py --precision mixed-shift
+  step "bench mixed" 300 $O/bench_mixed.json python bench.py --precision mixed
+  step "bench half-shift" 300 $O/bench_half_shift.json python bench.py --precision half-shift ;;
 karman) step "karman compute-only" 300 $O/karman_novtk.log python tools/bench_karman.py --iters 20000 --vtk 0 ;;
 prof) step "rocprof mixed-shift" 400 $O/prof_mixed_shift.log rocprofv3 --kernel-trace --stats -d $O/prof_mixed_shift -o run --output-format csv -- python3 $R/bench.py --steps 10 --warmup 2 --precision mixed-shift ;;
 counters)
@@ -39,5 +39,12 @@ dist)
   step "slab loopback overlap, pack kernels" 300 $O/dist_loop_overlap_pack.json env TCLB_HALO_MIRROR=0 python bench.py --shape 512,512,64 --steps 200 --warmup 20 --loopback-dist
   step "rocprof loopback overlap" 400 $O/prof_loop.log rocprofv3 --kernel-trace --stats -d $O/prof_loop -o run --output-format csv -- python3 $R/bench.py --shape 512,512,64 --steps 20 --warmup 5 --loopback-dist ;;
 pfms) step "pf384 storage modes" 600 $O/configs_pf_modes.log bash -c 'for p in double mixed-shift; do python tools/bench_configs.py --configs pf384,cavity --precision $p; done' ;;
-configs) step "configs" 400 $O/configs_r02c.log python tools/bench_configs.py ;;
+configs) step "configs" 400 $O/configs.log python tools/bench_configs.py ;;
+probe)
+  step "stream probe" 300 $O/stream_probe.log python tools/stream_probe.py
+  step "bench fp64 a" 300 $O/bench_fp64_a.json python bench.py
+  step "bench fp64 pad 2112" 300 $O/bench_fp64_pad2112.json env TCLB_FIELD_PAD=2112 python bench.py
+  step "bench fp64 b" 300 $O/bench_fp64_b.json python bench.py ;;
+smoke) step "smoke" 300 $O/smoke.log python -c "import __graft_entry__ as g; g.smoke()" ;;
+bench1) step "bench fp64" 300 $O/bench_fp64.json python bench.py ;;
 esac; done

@@ -234,3 +234,77 @@ def test_neumann_flux_q27_increment_moments():
             for c in range(3):
                 mom = np.tensordot(C[:, 0] ** a * C[:, 1] ** b * C[:, 2] ** c, d, 1)
                 np.testing.assert_allclose(mom, expect.get((a, b, c), 0.0), atol=1e-15, err_msg=str((a, b, c)))
+
+
+def _central_matrix(C, u):
+    """A[(a, b, c), i] = prod_d (C[i, d] - u[d])^(exponent d), exponents a + 3 b + 9 c"""
+    P = [(a, b, c) for c in range(3) for b in range(3) for a in range(3)]
+    return np.array([[np.prod([(C[i, d] - u[d]) ** p[d] for d in range(3)]) for i in range(len(C))] for p in P]), P
+
+
+def _oracle_q27(collision, h, C, om, uhyd, s2=1 / 3):
+    """post-collision h of relax_and_collide_ADE_CM_HIGHER_PROB[_M_EQ], written from the
+    reference formulas (models/heat/d3q27q27_cm_cht/Dynamics.c.Rt:1799-1831, 2008-2047):
+    central moments about u_h = m1 / m0, odd orders relax with omega, even ones take the
+    equilibrium; PROB returns about the blend u_hydro omega + u_h (1 - omega) with the
+    z component blended from u_hydro.y, M_EQ about u_h with the equilibrium moving with
+    du = u_hydro - u_h"""
+    H = h.sum()
+    uh = np.array([C[:, 0] @ h, C[:, 1] @ h, C[:, 2] @ h]) / H
+    A, P = _central_matrix(C, uh)
+    k = A @ h
+    out = np.empty(27)
+    du = uhyd - uh
+    for q, p in enumerate(P):
+        order = sum(p)
+        if collision == "CM_HIGHER_PROB":
+            eq = 0.0 if 1 in p else H * s2 ** sum(1 for e in p if e == 2)
+        else:
+            f = [1.0 if e == 0 else du[d] if e == 1 else s2 + du[d] ** 2 for d, e in enumerate(p)]
+            eq = H * np.prod(f)
+        if order % 2 == 1:
+            out[q] = (1 - om) * k[q] + (om * eq if collision == "CM_HIGHER_PROB_M_EQ" else 0.0)
+        else:
+            out[q] = eq
+    if collision == "CM_HIGHER_PROB":
+        back = np.array([om * uhyd[0] + (1 - om) * uh[0], om * uhyd[1] + (1 - om) * uh[1],
+                         om * uhyd[1] + (1 - om) * uh[2]])
+    else:
+        back = uh
+    B, _ = _central_matrix(C, back)
+    return np.linalg.solve(B, out)
+
+
+@pytest.mark.parametrize("collision", ["CM_HIGHER_PROB", "CM_HIGHER_PROB_M_EQ"])
+def test_q27_collision_with_moving_fluid(collision):
+    """uniform periodic state with a moving fluid (u = (0.03, -0.02, 0.05)) and perturbed h:
+    one step leaves every node at the post-collision h, which must equal an independent
+    NumPy transcription of the reference formulas (exercises the u_hydro blend, including
+    the reference's u_hydro.y in the z component, and the du-shifted equilibrium)"""
+    k = 0.07
+    U = np.array([0.03, -0.02, 0.05])
+    lat = _lat((4, 4, 4), collision, model="d3q27q27_cm_cht", nu=0.1, conductivity=k, InitTemperature=1.0,
+               VelocityX=U[0], VelocityY=U[1], VelocityZ=U[2])
+    m = lat.model
+    dens = [d for d in m.densities if d.field.group == "h"]
+    hi = [m.fields.index(d.field) for d in dens]
+    C = np.array([[d.dx, d.dy, d.dz] for d in dens], dtype=float)
+    f = lat.fields_interior().clone()
+    rng = np.random.default_rng(3)
+    pert = 1 + 0.2 * rng.standard_normal(27)
+    h0 = f[hi][:, 0, 0, 0].double().numpy() * pert
+    f[hi] = torch.as_tensor(h0, dtype=f.dtype)[:, None, None, None].expand(-1, *f.shape[1:]).clone()
+    lat.set_fields_interior(f)
+    gi = [m.fields.index(d.field) for d in m.densities if d.field.group == "f"]
+    Cg = np.array([[d.dx, d.dy, d.dz] for d in m.densities if d.field.group == "f"], dtype=float)
+    g = f[gi][:, 0, 0, 0].double().numpy()
+    uhyd = Cg.T @ g / g.sum()
+    np.testing.assert_allclose(uhyd, U, atol=1e-12)
+    lat.iterate(1)
+    h1 = lat.fields_interior()[hi].double().numpy()
+    expect = _oracle_q27(collision, h0, C, 1 / (3 * k + 0.5), uhyd)
+    assert np.abs(h1 - expect[:, None, None, None]).max() < 1e-13, (h1[:, 0, 0, 0], expect)
+    # the blend / moving equilibrium matters: a plain CM_HIGHER step gives another result
+    plain = _oracle_q27("CM_HIGHER_PROB", h0, C, 1 / (3 * k + 0.5), np.array([uhyd[0], uhyd[1], uhyd[2]]))
+    if collision == "CM_HIGHER_PROB_M_EQ":
+        assert np.abs(plain - expect).max() > 1e-6

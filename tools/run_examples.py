@@ -44,7 +44,63 @@ def model_from_header(path: str):
             name = m.group(1)
             if registry.exists(name):
                 return name
+    # no header: cases kept in a directory named after their model
+    # (example/multiphase/d3q27_pf_velocity/..., example/heat/d2q9q9_cm_cht/...)
+    for part in reversed(os.path.normpath(os.path.dirname(os.path.abspath(path))).split(os.sep)):
+        if registry.exists(part):
+            return part
     return None
+
+
+_GEOM_KEYWORDS = {"None", "Zone"}
+
+
+def case_requirements(path: str):
+    """(dims, node types drawn in <Geometry>, setting names set by <Param>/<Params>) of a case"""
+    from tclb_amd.utils.xpath import load_case
+    root = load_case(path)
+    dims, types, params = 2, set(), set()
+    for g in root.iter("Geometry"):
+        nz = re.match(r"\s*([0-9.]+)", g.get("nz", "1"))
+        if g.get("nz") is not None and not (nz and float(nz.group(1)) <= 1 and g.get("nz").strip() in ("1", "1.0")):
+            dims = 3
+        for ch in g:
+            if isinstance(ch.tag, str) and ch.tag not in _GEOM_KEYWORDS:
+                types.add(ch.tag)
+    units = {id(p) for u in root.iter("Units") for p in u.iter("Param")}
+    for p in root.iter("Param"):
+        if p.get("name") and id(p) not in units:
+            params.add(p.get("name"))
+    for p in root.iter("Params"):
+        for k in p.attrib:
+            params.add(k.split("-")[0])
+    return dims, types, params
+
+
+def infer_models(path: str, candidates=None, with_missing=False):
+    """reference-catalog models that accept the node types and settings the case uses, best
+    first: fewest unknown names, then fewest options.  Cases without a MODEL header are
+    run this way; the reference leaves the choice to the user (it builds every model and
+    the case names none)."""
+    from tclb_amd.models import registry
+    dims, types, params = case_requirements(path)
+    out = []
+    for name in candidates or registry.names():
+        try:
+            m = registry.get(name)
+        except Exception:  # noqa: BLE001 (a catalog entry that cannot be described)
+            continue
+        if m.dims != dims:
+            continue
+        nt = {n.name for n in m.node_types} | {n.group for n in m.node_types}
+        st = {s.name for s in m.settings} | {g.name + "InObj" for g in m.globals_}
+        missing = sorted((types - nt) | (params - st))
+        out.append((len(missing), len(name), name, missing))
+    out.sort()
+    if with_missing:
+        return [(n, miss) for _, _, n, miss in out]
+    best = out[0][0] if out else 0
+    return [n for k, _, n, _ in out if k == best]
 
 
 def capped_case(path: str, iters: int, outdir: str) -> str:
@@ -70,6 +126,9 @@ def main():
     ap.add_argument("--device", default="cpu")
     ap.add_argument("--out", default="/tmp/tclb_examples")
     ap.add_argument("--timeout", type=int, default=1200)
+    ap.add_argument("--infer", action="store_true",
+                    help="cases naming no model: pick the simplest catalog model that accepts every node type "
+                         "and setting the case uses")
     ap.add_argument("--cwd", default=None, help="working directory (default: the case's directory; the "
                                                  "reference resolves data paths like example/... from its root)")
     a = ap.parse_args()
@@ -77,12 +136,24 @@ def main():
     for case in a.cases:
         model = a.model or model_from_header(case)
         rec = {"case": case, "model": model}
+        with open(case, errors="replace") as f:
+            text = f.read()
+        if text.lstrip().startswith("<?R"):
+            # R-templated case (<?R ... ?> blocks): the reference expands it with its RT tool first
+            rec["status"] = "skipped: RT template, not a case"
+            print(json.dumps(rec), flush=True)
+            continue
+        if model is None and a.infer:
+            try:
+                fits = infer_models(case)
+            except Exception as e:  # noqa: BLE001 (an unparsable case is reported, not fatal)
+                fits, rec["error"] = [], str(e)[-300:]
+            model = fits[0] if fits else None
+            rec.update(model=model, inferred=fits[:5])
         if model is None:
             rec["status"] = "no model in header"
             print(json.dumps(rec), flush=True)
             continue
-        with open(case, errors="replace") as f:
-            text = f.read()
         if re.search(r"<\s*(RunR|RunPython)\b", text):
             # cases embedding R/Python code: the code in the case file is not executed here
             rec["status"] = "skipped: embedded RunR/RunPython code"
