@@ -426,6 +426,29 @@ def build_all(models: Optional[List[str]] = None, kinds=("cpu", "hip"), jobs: in
     return res
 
 
+def build_adjoint_libs(models: Optional[List[str]] = None, jobs: int = 0, force=False,
+                       verbose=False) -> Dict[str, Dict[str, str]]:
+    """dual-number adjoint executors (CPU "ad" and GPU "adhip") of the reference's ADJOINT=1
+    models plus d2q9_kuper (the two-stage stencil model of the GPU adjoint test), so GPU
+    runs load prebuilt libraries instead of compiling them on first use"""
+    from .models.dsl import ADJOINT_MODELS
+    models = models or sorted(ADJOINT_MODELS | {"d2q9_kuper"})
+    kinds = ("ad", "adhip") if os.path.exists(HIPCC) else ("ad",)
+    jobs = jobs or max(1, min(8, os.cpu_count() or 1))
+    for m in models:
+        emit_model(registry.get(m))
+
+    def one(t):
+        m, k = t
+        return m, k, build_model(m, kinds=(k,), force=force, verbose=verbose).get(k)
+
+    res: Dict[str, Dict[str, str]] = {m: {} for m in models}
+    with ThreadPoolExecutor(max_workers=jobs) as ex:
+        for m, k, p in ex.map(one, [(m, k) for m in models for k in kinds]):
+            res[m][k] = p
+    return res
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser(description="build tclb_amd model kernels")
     ap.add_argument("models", nargs="*")

@@ -10,18 +10,28 @@
 // code in scratch (K+1 doubles each).  Instead each thread re-runs its node in passes of
 // TCLB_AD_WINDOW tangents: pass p seeds only the inputs whose first-read index falls in
 // [p W, (p+1) W).  The first-read order is the same in every pass (identical primal
-// values, identical branches), so the passes partition the Jacobian columns; the thread
-// stops after the pass that covers the last input it saw.
+// values, identical branches), so the passes partition the Jacobian columns.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <utility>
 #include "tclb/ad.hpp"
 
 #ifndef TCLB_AD_WINDOW
-#define TCLB_AD_WINDOW 4
+#define TCLB_AD_WINDOW 3   // d3q19_adj: W = 3 keeps the node in 256 VGPRs, W = 4 spills to scratch
 #endif
 
 namespace tclb {
+
+// first-read keys of a thread's inputs live in LDS, interleaved across the 64 threads of
+// a k_ad block (key j of thread t at [j * 64 + t]: conflict-free).  Kept in the node
+// object, their runtime-indexed array would pin the whole node (populations, settings,
+// the Launch fields it copies) in scratch: SROA cannot split an object that has a
+// variable-offset access.
+constexpr int AD_BLOCK = 64;
+__device__ inline long long* ad_key_slot() {
+  __shared__ long long keys[TCLB_AD_K * AD_BLOCK];
+  return keys + threadIdx.x;
+}
 
 template <class T, int C>
 struct AdRec<Dual<T, C>> {
@@ -30,32 +40,34 @@ struct AdRec<Dual<T, C>> {
   AdCtx* ctx;
   long long fs, zp;
   int n, base;
-  long long key[KMAX];   // first-read order of the inputs: kind<<60 | field<<44 | index
+  long long* key;        // first-read order of the inputs: kind<<60 | field<<44 | index (LDS)
   TCLB_FN void init(const Launch& L) {
+    key = ad_key_slot();
     ctx = (AdCtx*)L.ext[5];
     fs = L.fs;
     zp = L.nzones;
     n = 0;
     base = L.reserved2;
+    for (int c = 0; c < C; c++) acc[c] = 0.0;
   }
   TCLB_FN static long long mk(int kind, int f, long long i) {
     return ((long long)kind << 60) | ((long long)f << 44) | i;
   }
   TCLB_FN D mark(double v, int j) const {
     D r(v);
-    if (j >= base && j < base + C) r.d[j - base] = T(1);
+    for (int c = 0; c < C; c++) r.d[c] = (j - base == c) ? T(1) : T(0);   // no runtime index
     return r;
   }
   TCLB_FN int find(long long k) const {
     for (int j = 0; j < n; j++)
-      if (key[j] == k) return j;
+      if (key[j * AD_BLOCK] == k) return j;
     return -1;
   }
   TCLB_FN D seed(double v, long long k) {
     const int j = find(k);
     if (j >= 0) return mark(v, j);
     if (n < KMAX) {
-      key[n] = k;
+      key[n * AD_BLOCK] = k;
       return mark(v, n++);
     }
     ctx->overflow = 1;
@@ -68,14 +80,22 @@ struct AdRec<Dual<T, C>> {
   TCLB_FN D zonal(int i, int zone, D v) {
     return (ctx && ctx->zon_mask && ctx->zon_mask[i]) ? seed(v.v, mk(2, i, zone)) : v;
   }
+  // the stage outputs' adjoints are contracted with this pass's tangents in registers
+  // (acc[c] = sum over stores of aout * d out / d input_(base+c)) and pushed with one
+  // atomic per input at the end of the pass (flush), instead of one atomic per
+  // (output, input) pair of the local Jacobian
+  double acc[C];
   TCLB_FN void scatter(double a, const D& val) {
     if (a == 0.0) return;
+    for (int c = 0; c < C; c++) acc[c] += a * (double)val.d[c];
+  }
+  TCLB_FN void flush() {
     for (int c = 0; c < C; c++) {
       const int j = base + c;
-      if (j >= n) break;
-      const double d = a * (double)val.d[c];
-      if (d == 0.0) continue;
-      const long long k = key[j];
+      const double d = acc[c];
+      acc[c] = 0.0;
+      if (j >= n || d == 0.0) continue;
+      const long long k = key[j * AD_BLOCK];
       const int kind = (int)(k >> 60), f = (int)((k >> 44) & 0xffff);
       const long long i = k & ((1LL << 44) - 1);
       double* dst = kind == 0 ? ctx->ain + (long long)f * fs + i
@@ -90,8 +110,14 @@ struct AdRec<Dual<T, C>> {
 
 namespace exec {
 
+// One launch per tangent window (L.reserved2 = first input of the window, set by the
+// host loop in ad_hip_impl).  Passes as separate launches rather than a loop in the
+// kernel: inside one kernel the compiler keeps the primal values of every pass live
+// and the d3q19_adj node spills to scratch (636 B/lane); one pass per launch needs no
+// scratch at W = 3.  The price: every node runs all K / W passes, also past the last
+// input it reads.
 template <class Model, int STG>
-__global__ void __launch_bounds__(64) k_ad(const Launch L, AdCtx* ctx) {
+__global__ void __launch_bounds__(AD_BLOCK) k_ad(const Launch L) {
   typedef Dual<double, TCLB_AD_WINDOW> D;
   constexpr int NG = Model::NGLOBALS_;
   constexpr int NSUM = Model::NSUMGLOBALS_;
@@ -99,28 +125,28 @@ __global__ void __launch_bounds__(64) k_ad(const Launch L, AdCtx* ctx) {
   const int y = L.ylo + (int)blockIdx.y;
   const int z = L.zlo + (int)blockIdx.z;
   if (x >= L.xhi) return;
-  Launch L2 = L;
-  L2.ext[5] = ctx;
-  for (int base = 0; base < TCLB_AD_K; base += TCLB_AD_WINDOW) {
-    L2.reserved2 = base;
-    D g[NG];
-    for (int i = 0; i < NG; i++) g[i] = i < NSUM ? D(0.0) : D(-1e30);
-    typename Model::template NodeT<D, double, true> nd(L2, x, y, z, g);
-    nd.template run_stage<STG>();
-    if (ctx->obj_weight != 0.0) nd.ad_.scatter(ctx->obj_weight, g[Model::OBJ_]);
-    if (base + TCLB_AD_WINDOW >= nd.ad_.n) break;   // every input seen has had its pass
-  }
+  D g[NG];
+  for (int i = 0; i < NG; i++) g[i] = i < NSUM ? D(0.0) : D(-1e30);
+  typename Model::template NodeT<D, double, true> nd(L, x, y, z, g);
+  nd.template run_stage<STG>();
+  const AdCtx* ctx = (const AdCtx*)L.ext[5];
+  if (ctx->obj_weight != 0.0) nd.ad_.scatter(ctx->obj_weight, g[Model::OBJ_]);
+  nd.ad_.flush();
 }
 
 template <class Model, int... I>
-inline int ad_hip_impl(const Launch& L, AdCtx* ctx, std::integer_sequence<int, I...>) {
+inline int ad_hip_impl(const Launch& L, std::integer_sequence<int, I...>) {
   const int w = L.xhi - L.xlo, h = L.yhi - L.ylo, d = L.zhi - L.zlo;
   if (w <= 0 || h <= 0 || d <= 0) return 0;
-  const dim3 grid((w + 63) / 64, h, d), block(64, 1, 1);
+  const dim3 grid((w + AD_BLOCK - 1) / AD_BLOCK, h, d), block(AD_BLOCK, 1, 1);
   hipStream_t s = (hipStream_t)L.stream;
-  bool found = false;
-  ((L.stage == I ? (k_ad<Model, I><<<grid, block, 0, s>>>(L, ctx), found = true) : false), ...);
-  if (!found) return -2;
+  for (int base = 0; base < TCLB_AD_K; base += TCLB_AD_WINDOW) {
+    Launch Lb = L;
+    Lb.reserved2 = base;
+    bool found = false;
+    ((L.stage == I ? (k_ad<Model, I><<<grid, block, 0, s>>>(Lb), found = true) : false), ...);
+    if (!found) return -2;
+  }
   return (int)hipGetLastError();
 }
 
@@ -130,8 +156,7 @@ inline int ad_hip_impl(const Launch& L, AdCtx* ctx, std::integer_sequence<int, I
 // ctx: device copy of the AdCtx (aout/ain/gset/gzon/masks are device pointers)
 #define TCLB_EXPORT_AD_HIP(NAME, MODEL)                                                      \
   extern "C" int tclb_##NAME##_adjoint(const tclb::Launch* L) {                              \
-    return tclb::exec::ad_hip_impl<MODEL>(*L, (tclb::AdCtx*)L->ext[5],                       \
-                                          std::make_integer_sequence<int, MODEL::NSTAGES_>{}); \
+    return tclb::exec::ad_hip_impl<MODEL>(*L, std::make_integer_sequence<int, MODEL::NSTAGES_>{}); \
   }                                                                                          \
   extern "C" int tclb_##NAME##_ad_tangents() { return TCLB_AD_K; }                           \
   extern "C" int tclb_##NAME##_ad_device() { return 1; }                                     \

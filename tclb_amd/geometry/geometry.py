@@ -362,7 +362,9 @@ class Geometry:
                     raise GeometryError(f"Unknown geometry element: {tag}")
 
     def _axis_pipe(self, n, reg, ax):
-        x0, y0, z0 = (self._attr_f(n, a) for a in "xyz")
+        # the coordinate along the pipe axis is read but unused by the reference
+        # (src/Geometry.cpp.Rt:872): cases omit it (annularTaylorBubble_DasC.xml XPipe)
+        x0, y0, z0 = (self._attr_f(n, a, 0.0 if a == ax.lower() else None) for a in "xyz")
         other = {"X": ("y", "z"), "Y": ("x", "z"), "Z": ("x", "y")}[ax]
         if n.get("R") is None:
             Ra, Rb = self._attr_f(n, "R" + other[0]), self._attr_f(n, "R" + other[1])
