@@ -50,6 +50,7 @@ class Adjoint:
         self.series_grads = {}
         self.ctx = abi.AdCtx()
         # the GPU executor reads its context from device memory
+        self._ad_cover = {}   # stage -> largest input count of a node (GPU pass sizing)
         self._ctx_dev = torch.zeros(ctypes.sizeof(abi.AdCtx), dtype=torch.uint8, device=dev) if lat.is_gpu else None
 
     # ------------------------------------------------------------------ one action
@@ -94,7 +95,12 @@ class Adjoint:
         c.zon_mask = self.zon_mask.data_ptr()
         c.obj_weight = obj_weight
         c.overflow = 0
+        c.reserved = 0
         L.reserved2 = 0
+        # GPU: tangent windows up to the largest input count a node of this stage read in an
+        # earlier call (0 = all TCLB_AD_K); the device reports the count in AdCtx.reserved
+        cover = self._ad_cover.get(si, 0) if self._ctx_dev is not None else 0
+        L.reserved0 = cover
         L.stream = lat._stream()
         if self._ctx_dev is not None:
             self._ctx_dev.copy_(torch.frombuffer(bytearray(bytes(c)), dtype=torch.uint8))
@@ -111,6 +117,15 @@ class Adjoint:
         self.lib.run(L)
         if self._ctx_dev is not None:
             c = abi.AdCtx.from_buffer_copy(bytes(self._ctx_dev.cpu().numpy()))
+            w = self.lib.window
+            covered = -(-cover // w) * w if cover else self.lib.tangents
+            if c.reserved > covered:
+                # a node read more inputs than the windows covered: the windows partition the
+                # Jacobian columns, so the missing ones are added by the remaining windows
+                L.reserved2, L.reserved0 = covered, 0
+                self.lib.run(L)
+                c = abi.AdCtx.from_buffer_copy(bytes(self._ctx_dev.cpu().numpy()))
+            self._ad_cover[si] = max(cover, c.reserved)
         if c.overflow:
             raise AdjointError(f"model {lat.model.name}: a node needed more than {self.lib.tangents} AD tangents")
         self._fold_ghosts(ain)

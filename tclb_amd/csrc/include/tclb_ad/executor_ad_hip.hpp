@@ -114,8 +114,8 @@ namespace exec {
 // host loop in ad_hip_impl).  Passes as separate launches rather than a loop in the
 // kernel: inside one kernel the compiler keeps the primal values of every pass live
 // and the d3q19_adj node spills to scratch (636 B/lane); one pass per launch needs no
-// scratch at W = 3.  The price: every node runs all K / W passes, also past the last
-// input it reads.
+// scratch at W = 3.  Every node runs the passes of the launch; after the first call of a
+// stage the host covers only the largest input count seen (adjoint.py), not all K.
 template <class Model, int STG>
 __global__ void __launch_bounds__(AD_BLOCK) k_ad(const Launch L) {
   typedef Dual<double, TCLB_AD_WINDOW> D;
@@ -124,14 +124,23 @@ __global__ void __launch_bounds__(AD_BLOCK) k_ad(const Launch L) {
   const int x = L.xlo + (int)(blockIdx.x * blockDim.x + threadIdx.x);
   const int y = L.ylo + (int)blockIdx.y;
   const int z = L.zlo + (int)blockIdx.z;
-  if (x >= L.xhi) return;
-  D g[NG];
-  for (int i = 0; i < NG; i++) g[i] = i < NSUM ? D(0.0) : D(-1e30);
-  typename Model::template NodeT<D, double, true> nd(L, x, y, z, g);
-  nd.template run_stage<STG>();
-  const AdCtx* ctx = (const AdCtx*)L.ext[5];
-  if (ctx->obj_weight != 0.0) nd.ad_.scatter(ctx->obj_weight, g[Model::OBJ_]);
-  nd.ad_.flush();
+  AdCtx* ctx = (AdCtx*)L.ext[5];
+  int n = 0;
+  if (x < L.xhi) {
+    D g[NG];
+    for (int i = 0; i < NG; i++) g[i] = i < NSUM ? D(0.0) : D(-1e30);
+    typename Model::template NodeT<D, double, true> nd(L, x, y, z, g);
+    nd.template run_stage<STG>();
+    if (ctx->obj_weight != 0.0) nd.ad_.scatter(ctx->obj_weight, g[Model::OBJ_]);
+    nd.ad_.flush();
+    n = nd.ad_.n;
+  }
+  // first pass: the largest input count of the launch (ctx->reserved), from which the
+  // host sizes the passes of later calls of this stage (AdCtx.reserved, adjoint.py)
+  if (L.reserved2 == 0) {
+    for (int off = AD_BLOCK / 2; off > 0; off >>= 1) n = max(n, __shfl_xor(n, off));
+    if (threadIdx.x == 0 && n > 0) atomicMax(&ctx->reserved, n);
+  }
 }
 
 template <class Model, int... I>
@@ -140,7 +149,9 @@ inline int ad_hip_impl(const Launch& L, std::integer_sequence<int, I...>) {
   if (w <= 0 || h <= 0 || d <= 0) return 0;
   const dim3 grid((w + AD_BLOCK - 1) / AD_BLOCK, h, d), block(AD_BLOCK, 1, 1);
   hipStream_t s = (hipStream_t)L.stream;
-  for (int base = 0; base < TCLB_AD_K; base += TCLB_AD_WINDOW) {
+  // windows [L.reserved2, L.reserved0) of the input list (reserved0 = 0: all TCLB_AD_K)
+  const int end = (L.reserved0 > 0 && L.reserved0 < TCLB_AD_K) ? L.reserved0 : TCLB_AD_K;
+  for (int base = L.reserved2; base < end; base += TCLB_AD_WINDOW) {
     Launch Lb = L;
     Lb.reserved2 = base;
     bool found = false;
@@ -159,5 +170,6 @@ inline int ad_hip_impl(const Launch& L, std::integer_sequence<int, I...>) {
     return tclb::exec::ad_hip_impl<MODEL>(*L, std::make_integer_sequence<int, MODEL::NSTAGES_>{}); \
   }                                                                                          \
   extern "C" int tclb_##NAME##_ad_tangents() { return TCLB_AD_K; }                           \
+  extern "C" int tclb_##NAME##_ad_window() { return TCLB_AD_WINDOW; }                        \
   extern "C" int tclb_##NAME##_ad_device() { return 1; }                                     \
   extern "C" int tclb_##NAME##_sizeof_launch() { return (int)sizeof(tclb::Launch); }

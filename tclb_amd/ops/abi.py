@@ -124,6 +124,9 @@ class AdLib:
         self._adj.argtypes = [ctypes.POINTER(Launch)]
         self._adj.restype = ctypes.c_int
         self.tangents = getattr(self.lib, f"tclb_{model}_ad_tangents")()
+        # GPU executor: tangents per pass (TCLB_AD_WINDOW); the CPU executor carries all at once
+        win = getattr(self.lib, f"tclb_{model}_ad_window", None)
+        self.window = win() if win is not None else self.tangents
         sz = getattr(self.lib, f"tclb_{model}_sizeof_launch")()
         if sz != ctypes.sizeof(Launch):
             raise KernelError(f"ABI mismatch for {path}")
