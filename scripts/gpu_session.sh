@@ -45,6 +45,10 @@ probe)
   step "bench fp64 a" 300 $O/bench_fp64_a.json python bench.py
   step "bench fp64 pad 2112" 300 $O/bench_fp64_pad2112.json env TCLB_FIELD_PAD=2112 python bench.py
   step "bench fp64 b" 300 $O/bench_fp64_b.json python bench.py ;;
+adwin)
+  for v in "" w1 w2 w4; do
+    step "adjoint bench 128 window ${v:-w3}" 300 $O/bench_adjoint_128_${v:-w3}.json env TCLB_AD_VARIANT=$v python tools/bench_adjoint.py --size 128 --steps 80
+  done ;;
 smoke) step "smoke" 300 $O/smoke.log python -c "import __graft_entry__ as g; g.smoke()" ;;
 bench1) step "bench fp64" 300 $O/bench_fp64.json python bench.py ;;
 esac; done

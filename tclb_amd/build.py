@@ -48,9 +48,13 @@ CPU_VARIANTS = {
 }
 
 
+# GPU adjoint executor variants: tangents per pass (tclb_ad/executor_ad_hip.hpp TCLB_AD_WINDOW)
+AD_VARIANTS = {f"w{w}": [f"-DTCLB_AD_WINDOW={w}"] for w in (1, 2, 3, 5)}
+
+
 def _variant_of(kind: str, variant: str) -> str:
     """the variant a library of this kind is built in ("" for kinds without variants)"""
-    if kind == "hip" or (kind == "cpu" and variant in CPU_VARIANTS):
+    if kind == "hip" or (kind == "cpu" and variant in CPU_VARIANTS) or (kind == "adhip" and variant in AD_VARIANTS):
         return variant
     return ""
 
@@ -116,7 +120,7 @@ def _cmd(kind: str, src: str, out: str, gen_dir: str, variant: str = "") -> List
     incs = ["-I", os.path.join(CSRC, "include"), "-I", os.path.join(CSRC, "models"), "-I", gen_dir]
     if kind == "adhip":
         return [HIPCC, f"--offload-arch={ARCH}", "-O2", "-std=c++17", "-fPIC", "-shared", "-munsafe-fp-atomics",
-                "-Wno-unused-result", "-Wno-pass-failed", *incs, src, "-o", out]
+                "-Wno-unused-result", "-Wno-pass-failed", *AD_VARIANTS.get(variant, []), *incs, src, "-o", out]
     if kind == "hip":
         # simplifycfg-sink-common=false: boundary-condition switch cases that permute
         # the population array differ only in constant indices; sinking them into one

@@ -17,7 +17,9 @@
 #include "tclb/ad.hpp"
 
 #ifndef TCLB_AD_WINDOW
-#define TCLB_AD_WINDOW 3   // d3q19_adj: W = 3 keeps the node in 256 VGPRs, W = 4 spills to scratch
+// d3q19_adj 128^3 (profiles/r02o): W = 4 10.2 ms per adjoint step (268 B/lane of spills),
+// W = 3 11.9 ms (no scratch), W = 2 14.3, W = 1 15.1; W = 5 spills 752 B/lane
+#define TCLB_AD_WINDOW 4
 #endif
 
 namespace tclb {
@@ -113,9 +115,10 @@ namespace exec {
 // One launch per tangent window (L.reserved2 = first input of the window, set by the
 // host loop in ad_hip_impl).  Passes as separate launches rather than a loop in the
 // kernel: inside one kernel the compiler keeps the primal values of every pass live
-// and the d3q19_adj node spills to scratch (636 B/lane); one pass per launch needs no
-// scratch at W = 3.  Every node runs the passes of the launch; after the first call of a
-// stage the host covers only the largest input count seen (adjoint.py), not all K.
+// and the d3q19_adj node spills 636 B/lane at W = 3; one pass per launch needs no
+// scratch at W = 3 (268 B/lane of spills at the default W = 4).  Every node runs the
+// passes of the launch; after the first call of a stage the host covers only the
+// largest input count seen (adjoint.py), not all K.
 template <class Model, int STG>
 __global__ void __launch_bounds__(AD_BLOCK) k_ad(const Launch L) {
   typedef Dual<double, TCLB_AD_WINDOW> D;

@@ -140,16 +140,18 @@ class AdLib:
 def load_ad(model: str, gpu: bool = False) -> AdLib:
     from .. import build as B
     kind = "adhip" if gpu else "ad"
-    key = (model, kind, "")
+    # TCLB_AD_VARIANT: tangent-window build of the GPU executor (build.AD_VARIANTS, A/B only)
+    variant = os.environ.get("TCLB_AD_VARIANT", "") if gpu else ""
+    key = (model, kind, variant)
     with _lock:
         if key in _libs:
             return _libs[key]
-        path = B.lib_path(model, kind)
-        stale = B.stale_reason(model, kind)
+        path = B.lib_path(model, kind, variant)
+        stale = B.stale_reason(model, kind, variant)
         if stale is not None:
             if os.environ.get("TCLB_NO_BUILD"):
                 raise KernelError(f"adjoint library for model '{model}' [{kind}] is not usable ({stale}): {path}")
-            B.build_model(model, kinds=(kind,))
+            B.build_model(model, kinds=(kind,), variant=variant)
         if not os.path.exists(path):
             raise KernelError(f"adjoint library for model '{model}' [{kind}] not built: {path}")
         lib = AdLib(model, path, kind)
