@@ -5,7 +5,7 @@
 
 The model of a case is read from its header comment (``MODEL: <name>``, ``Model: <name>``,
 ``To be used with <name>``, ``Run with <name> model``) or given with ``--model``.  Every
-``<Solve>`` / ``<RunAction>`` is capped to ``--iters`` iterations and ``<Repeat>`` to one
+``<Solve>`` / ``<RunAction>`` / ``<OptSolve>`` is capped to ``--iters`` iterations and ``<Repeat>`` to one
 pass, so the case runs its geometry, initialisation, handlers and output once.  Each case
 runs in a child process (``python -m tclb_amd <model> <case> <xpath edits>``) with the
 case's directory as working directory and the output directory redirected to ``--out``;
@@ -108,7 +108,7 @@ def capped_case(path: str, iters: int, outdir: str) -> str:
     root = load_case(path)
     root.set("output", outdir.rstrip("/") + "/")
     for el in root.iter():
-        if el.tag in ("Solve", "RunAction") and "Iterations" in el.attrib:
+        if el.tag in ("Solve", "RunAction", "OptSolve") and "Iterations" in el.attrib:
             el.set("Iterations", str(iters))
         if el.tag == "Repeat" and "Times" in el.attrib:
             el.set("Times", "1")
