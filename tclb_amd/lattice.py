@@ -308,10 +308,12 @@ class Lattice:
         if trace.ENABLED:
             trace.pop()
 
-    def _mirror_buffer(self, fields: List[int], axis: int) -> torch.Tensor:
+    def _mirror_buffer(self, fields: List[int], axis: int, side: str) -> torch.Tensor:
         """persistent packed halo buffer [len(fields)][g planes] of one side, laid out as
-        _pack's output (zeroed once, so the x pitch padding stays finite)"""
-        key = ("mirror", axis, tuple(fields))
+        _pack's output (zeroed once, so the x pitch padding stays finite).  The side is
+        part of the key: with a symmetric stencil the lo and hi field lists are equal,
+        and one shared buffer would carry the top planes in both directions."""
+        key = ("mirror", axis, side, tuple(fields))
         t = self._halo_bufs.get(key)
         if t is None:
             g = self.gz if axis == 2 else self.gy
@@ -356,8 +358,8 @@ class Lattice:
         fs = set(fields)
         lo = [i for i in lo_set if i in fs]        # read from below: my top planes go up
         hi = [i for i in hi_set if i in fs]        # read from above: my bottom planes go down
-        send_down = self._mirror_buffer(hi, axis) if hi else None
-        send_up = self._mirror_buffer(lo, axis) if lo else None
+        send_down = self._mirror_buffer(hi, axis, "down") if hi else None
+        send_up = self._mirror_buffer(lo, axis, "up") if lo else None
         if hi:
             self._launch_mirrored(stage, src, dst, glob, (0, g), hi, send_down, axis)
         else:

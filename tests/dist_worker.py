@@ -66,3 +66,33 @@ def worker(rank, world, port, model, shape, steps, out, overlap, grid=None):
             json.dump(parts[0][2], f)
     dist.barrier()
     dist.destroy_process_group()
+
+
+def worker_catalog(rank, world, port, model, steps, out, overlap, mirror="1"):
+    """any catalog model with the generic set-up of tests/model_cases.py (global-coordinate
+    perturbation), gathered to rank 0 as in worker()"""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    os.environ["TCLB_HALO_MIRROR"] = mirror
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from model_cases import make_case, perturb
+    from tclb_amd.parallel.comm import TorchDistComm
+    comm = TorchDistComm()
+    lat = make_case(model, "cpu", comm=comm)
+    lat.overlap = lat.overlap and overlap
+    lat.init()
+    perturb(lat)
+    lat.iterate(steps)
+    parts = comm.gather_objects((lat.slab.offset, lat.fields_interior().numpy(), lat.globals))
+    if rank == 0:
+        gnx, gny, gnz = lat.gshape
+        full = np.zeros((lat.nf, gnz, gny, gnx))
+        for (ox, oy, oz), a, _ in parts:
+            full[:, oz:oz + a.shape[1], oy:oy + a.shape[2], :] = a
+        np.save(out, full)
+        import json
+        with open(out + ".json", "w") as f:
+            json.dump(parts[0][2], f)
+    dist.barrier()
+    dist.destroy_process_group()
