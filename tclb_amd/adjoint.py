@@ -131,27 +131,29 @@ class Adjoint:
         self._fold_ghosts(ain)
         return ain
 
-    def step_back(self, a_next: torch.Tensor, action: str = "Iteration", obj_weight: float = 1.0) -> torch.Tensor:
-        """adjoint of one `action` applied to the current primal state (snapshot cur):
-        given a_next = dJ/d(state after the action) return dJ/d(state before), adding
-        this step's Objective derivative (weight obj_weight) and setting gradients."""
+    def step_back(self, a_next: torch.Tensor, action: str = "Iteration", obj_weight: float = 1.0,
+                  state: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """adjoint of one `action` applied to the primal state `state` (default: the
+        current snapshot): given a_next = dJ/d(state after the action) return
+        dJ/d(state before), adding this step's Objective derivative (weight obj_weight)
+        and setting gradients."""
         lat = self.lat
         m = lat.model
         act = m.action(action)
-        src = lat.snaps[lat.cur]
-        # forward recompute of the intermediate in-place states of multi-stage actions
+        src = lat.snaps[lat.cur] if state is None else state
+        # forward recompute of the intermediate in-place states of multi-stage actions,
+        # in a work copy of the other snapshot (fields a stage does not write keep what
+        # the output snapshot held, as in the primal step)
         inputs: List[torch.Tensor] = [src]
         if len(act.stages) > 1:
-            saved = lat.cur
-            tmp = lat.snaps[1 - lat.cur].clone()
             glob = lat.globals_t.clone()
-            dst = lat.snaps[1 - lat.cur]
+            other = lat.snaps[1 - lat.cur] if state is None else lat.snaps[lat.cur]
+            dst = other.clone()
             for k, sname in enumerate(act.stages[:-1]):
                 si = m.stage_index(sname)
                 lat._launch_stage(si, src if k == 0 else dst, dst, False)
                 lat._halo_finish(lat._halo_start(dst, lat._saved_fields(m.stage(sname))))
                 inputs.append(dst.clone())
-            lat.snaps[1 - saved].copy_(tmp)
             lat.globals_t.copy_(glob)
         a = a_next
         for k in range(len(act.stages) - 1, -1, -1):
@@ -225,7 +227,8 @@ class Adjoint:
     def param_fields(self) -> List[int]:
         return [i for i, f in enumerate(self.lat.model.fields) if f.parameter]
 
-    def steady_step(self, a: torch.Tensor, action: str = "Iteration") -> torch.Tensor:
+    def steady_step(self, a: torch.Tensor, action: str = "Iteration",
+                    state: Optional[torch.Tensor] = None) -> torch.Tensor:
         """one steady-adjoint iteration (reference SteadyAdjoint kernels, "SAdj" dispatch
         with zeropar, src/conf.R:831-839): the adjoint of the parameter densities is
         zeroed on entry, so on exit it holds this iteration's gradient contribution
@@ -236,7 +239,7 @@ class Adjoint:
             a[pf] = 0
         self.gset.zero_()
         self.gzon.zero_()
-        return self.step_back(a, action)
+        return self.step_back(a, action, state=state)
 
     def steady(self, iterations: int, action: str = "Iteration", tol: float = 0.0) -> torch.Tensor:
         """fixed-point adjoint at the current (converged) primal state: a <- A^T a + dJ/df"""

@@ -43,7 +43,8 @@ def save_state(solver, prefix: str) -> str:
             json.dump(hdr, f, indent=1)
     solver.comm.barrier()
     mm = np.load(path, mmap_mode="r+")
-    loc = lat.fields_interior().detach().cpu().numpy().astype(dt, copy=False)
+    # shifted storage: the shift is added in fp64 (a fp32 sum would round f - w around w)
+    loc = lat.fields_interior(torch.float64 if dt == np.float64 else None).detach().cpu().numpy().astype(dt, copy=False)
     ox, oy, oz = lat.slab.offset
     nx, ny, nz = lat.shape
     mm[:, oz:oz + nz, oy:oy + ny, :] = loc

@@ -666,14 +666,16 @@ class Lattice:
             return v.to(self.rdtype) + self._shift_t[i, 0].to(self.rdtype)
         return v
 
-    def fields_interior(self) -> torch.Tensor:
+    def fields_interior(self, dtype: Optional[torch.dtype] = None) -> torch.Tensor:
         """all fields on the interior (nf, nz, ny, nx): a view of the storage, or for the
-        *-shift precisions a copy with the storage shift added back"""
+        *-shift precisions a copy with the storage shift added back in `dtype` (default
+        the compute dtype; checkpoints ask for fp64 so that f - w round-trips exactly)"""
         nx, ny, nz = self.shape
         v = self.snaps[self.cur][:, self.gz:self.gz + nz, self.gy:self.gy + ny, :nx]
         if self._shift_t is not None:
-            return v.to(self.rdtype) + self._shift_t.to(self.rdtype)
-        return v
+            dt = dtype or self.rdtype
+            return v.to(dt) + self._shift_t.to(dt)
+        return v if dtype is None else v.to(dtype)
 
     def set_fields_interior(self, data: torch.Tensor):
         nx, ny, nz = self.shape

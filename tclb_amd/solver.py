@@ -139,8 +139,10 @@ class Solver:
         glob = bool(self.iter_type & (ITER_LASTGLOB | ITER_GLOBS))
         if self.iter_type & ITER_OPT:
             for k in range(steps):
+                # the primal step writes the other snapshot and leaves its input intact:
+                # after it, snaps[1 - cur] is the pre-step state the adjoint linearises at
                 lat.iterate(1, glob_last=glob and k == steps - 1, action=action or "Iteration")
-                self._opt_iteration(action or "Iteration")
+                self._opt_iteration(action or "Iteration", lat.snaps[1 - lat.cur])
             self.iter += steps
             self._speed_meter(steps)
             return
@@ -151,14 +153,16 @@ class Solver:
         self.iter += steps
         self._speed_meter(steps)
 
-    def _opt_iteration(self, action: str):
+    def _opt_iteration(self, action: str, pre_state):
         """the Optimize part of one ITER_OPT iteration (reference Lattice::<Action>_Opt,
         src/Lattice.cu.Rt:624-636 and the Opt() node function, src/cuda.cu.Rt:241-253):
-        one steady-adjoint step at the current primal state, then on DesignSpace nodes
-        every parameter density moves by Descent x its adjoint, clamped to [0, 1]"""
+        one steady-adjoint step linearised at the pre-step primal state (the reference's
+        Iteration_Adj(tab0, ...) after Iteration(tab0 -> tab1)), then on DesignSpace nodes
+        every parameter density of the new state moves by Descent x its adjoint, clamped
+        to [0, 1]"""
         lat = self.lattice
         ad = self.opt_adjoint
-        self.opt_state = ad.steady_step(self.opt_state, action)
+        self.opt_state = ad.steady_step(self.opt_state, action, state=pre_state)
         descent = lat.get_setting("Descent") if self.model.setting("Descent") is not None else 0.0
         pf = ad.param_fields()
         if not pf or descent == 0.0:

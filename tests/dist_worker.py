@@ -96,3 +96,40 @@ def worker_catalog(rank, world, port, model, steps, out, overlap, mirror="1"):
             json.dump(parts[0][2], f)
     dist.barrier()
     dist.destroy_process_group()
+
+
+def worker_checkpoint(rank, world, port, model, path, steps_before, steps_after, out):
+    """checkpoint round trip over a rank-count change: with steps_before > 0 run that many
+    steps and write `path`; then (steps_before == 0) load `path` and run steps_after,
+    gathering the fields to rank 0 (`out`)"""
+    import types
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from model_cases import make_case, perturb
+    from tclb_amd.io.checkpoint import load_state, save_state
+    from tclb_amd.parallel.comm import TorchDistComm
+    comm = TorchDistComm()
+    lat = make_case(model, "cpu", comm=comm)
+    lat.init()
+    solver = types.SimpleNamespace(lattice=lat, rank=rank, comm=comm, iter=0)
+    if steps_before > 0:
+        perturb(lat)
+        lat.iterate(steps_before)
+        solver.iter = lat.iter
+        save_state(solver, path)
+    else:
+        load_state(solver, path)
+        lat.iterate(steps_after)
+        parts = comm.gather_objects((lat.slab.offset, lat.fields_interior().numpy(), lat.iter))
+        if rank == 0:
+            gnx, gny, gnz = lat.gshape
+            full = np.zeros((lat.nf, gnz, gny, gnx))
+            for (ox, oy, oz), a, _ in parts:
+                full[:, oz:oz + a.shape[1], oy:oy + a.shape[2], :] = a
+            np.save(out, full)
+            with open(out + ".iter", "w") as f:
+                f.write(str(parts[0][2]))
+    dist.barrier()
+    dist.destroy_process_group()

@@ -89,3 +89,30 @@ def test_steady_step_parameter_gradient_is_local():
     g2 = a[wi]
     assert g1.abs().max() > 0
     assert (g2 - g1).abs().max() <= 1e-8 * g1.abs().max()
+
+
+def test_optsolve_linearises_at_pre_step_state(tmp_path):
+    """advisor r02: the ITER_OPT adjoint step must be taken at the pre-step primal state
+    (reference Iteration(tab0 -> tab1) then Iteration_Adj(tab0, ...)), and the design
+    update applied to the post-step state"""
+    import torch
+    from tclb_amd.adjoint import Adjoint
+    (tmp_path / "a").mkdir()
+    (tmp_path / "b").mkdir()
+    s_pre = _run(tmp_path / "a", 5.0, '<Solve Iterations="40"/>')
+    s_opt = _run(tmp_path / "b", 5.0, '<Solve Iterations="40"/><OptSolve Iterations="1"/>')
+    lat = s_pre.lattice
+    pre = lat.snaps[lat.cur].clone()
+    ad = Adjoint(lat)
+    a = ad.steady_step(torch.zeros_like(pre), state=None)        # linearised at the pre-step state
+    lat.iterate(1, glob_last=False)
+    post = lat.snaps[lat.cur]
+    assert torch.equal(lat.snaps[1 - lat.cur], pre)              # the primal step left its input intact
+    assert torch.equal(s_opt.opt_state, a)
+    # a linearisation at the post-step state differs (the primal is not converged)
+    b = ad.steady_step(torch.zeros_like(pre))
+    assert not torch.equal(a, b)
+    wi = lat.model.field_index("w")
+    ds = (s_opt.lattice.flags.to(torch.int64) & lat.model.group_masks["DESIGNSPACE"]) != 0
+    upd = torch.where(ds, (post[wi] + a[wi] * 5.0).clamp(0.0, 1.0), post[wi])
+    assert torch.equal(s_opt.lattice.snaps[s_opt.lattice.cur][wi], upd)
