@@ -81,3 +81,23 @@ def read_vti(path: str) -> Dict[str, np.ndarray]:
         a = a.reshape(nz, ny, nx, nc) if nc > 1 else a.reshape(nz, ny, nx)
         out[da.get("Name")] = a
     return out
+
+
+def read_pvti(path: str) -> Dict[str, np.ndarray]:
+    """assemble the pieces of a .pvti index into whole-extent arrays (tests, comparisons
+    of runs on different rank counts)"""
+    import xml.etree.ElementTree as ET
+    root = ET.parse(path).getroot()
+    img = root.find("PImageData")
+    w = [int(v) for v in img.get("WholeExtent").split()]
+    out: Dict[str, np.ndarray] = {}
+    base = os.path.dirname(path)
+    for piece in img.findall("Piece"):
+        e = [int(v) for v in piece.get("Extent").split()]
+        data = read_vti(os.path.join(base, piece.get("Source")))
+        for name, a in data.items():
+            if name not in out:
+                shape = (w[5] - w[4], w[3] - w[2], w[1] - w[0]) + a.shape[3:]
+                out[name] = np.zeros(shape, dtype=a.dtype)
+            out[name][e[4] - w[4]:e[5] - w[4], e[2] - w[2]:e[3] - w[2], e[0] - w[0]:e[1] - w[0]] = a
+    return out
