@@ -140,7 +140,8 @@ class Lattice:
         self.globals: Dict[str, float] = {g.name: 0.0 for g in m.globals_}
         self.iter = 0
         self.block = block
-        self.overlap = (self.comm.distributed if overlap is None else overlap) and ax != 3
+        self.overlap = self.comm.distributed if overlap is None else overlap
+        self._halo_stream = None          # side stream of the Y x Z grid's two-phase halo
         # overlapped steps pack their outgoing halo inside the border kernels (Launch.mbase);
         # TCLB_HALO_MIRROR=0 keeps the separate pack kernels (A/B)
         self.halo_mirror = os.environ.get("TCLB_HALO_MIRROR", "1") != "0"
@@ -208,7 +209,8 @@ class Lattice:
         return torch.cuda.current_stream(self.device).cuda_stream if self.is_gpu else 0
 
     def _launch_stage(self, stage: int, src: torch.Tensor, dst: torch.Tensor, glob: bool,
-                      axis_range: Optional[Tuple[int, int]] = None):
+                      axis_range: Optional[Tuple[int, int]] = None,
+                      box: Optional[Tuple[int, int, int, int]] = None):
         L = self._L
         L.in_ = src.data_ptr()
         L.out = dst.data_ptr()
@@ -224,6 +226,8 @@ class Lattice:
                 L.zlo, L.zhi = axis_range
             else:
                 L.ylo, L.yhi = axis_range
+        if box is not None:               # (ylo, yhi, zlo, zhi) of the Y x Z grid split
+            L.ylo, L.yhi, L.zlo, L.zhi = box
         self.lib.run(L, self.prec)
         if trace.SYNC:
             trace.after_launch(self, f"{self.model.name} stage {stage}")
@@ -378,6 +382,43 @@ class Lattice:
         h = self.comm.start_halo(send_up, send_down, recv_below, recv_above)
         return (h, dst, lo, hi, recv_below, recv_above, send_up, send_down, axis)
 
+    def _grid_overlapped(self, stage: int, src, dst, glob: bool, fields: List[int]):
+        """overlapped step of the Y x Z process grid: the four border slabs (z planes over
+        all y, then y rows over the inner z), then the two-phase halo (z planes, then y
+        rows over the ghost-inclusive z extent, which fills the edge ghosts) on a side
+        stream while the interior kernel runs.  Reference: RunBorder -> MPIStream_A ->
+        RunInterior -> MPIStream_B (src/Lattice.cu.Rt:466-533) over MPIDivision's grid."""
+        nx, ny, nz = self.shape
+        gy, gz = self.gy, self.gz
+        for box in ((0, ny, 0, gz), (0, ny, nz - gz, nz), (0, gy, gz, nz - gz), (ny - gy, ny, gz, nz - gz)):
+            self._launch_stage(stage, src, dst, glob, box=box)
+        if trace.ENABLED:
+            trace.push("halo")
+        done = None
+        if self.is_gpu:
+            # the halo packs/unpacks go on a side stream ordered after the border kernels,
+            # so the y phase (which waits for the z phase) never queues behind the interior
+            cur = torch.cuda.current_stream(self.device)
+            if self._halo_stream is None:
+                self._halo_stream = torch.cuda.Stream(self.device)
+            hs = self._halo_stream
+            hs.wait_stream(cur)
+            with torch.cuda.stream(hs):
+                for a in (2, 1):
+                    self._halo_finish(self._halo_axis_start(dst, fields, a))
+            done = torch.cuda.Event()
+            done.record(hs)
+        else:
+            hz = self._halo_axis_start(dst, fields, 2)
+        self._launch_stage(stage, src, dst, glob, box=(gy, ny - gy, gz, nz - gz))
+        if self.is_gpu:
+            torch.cuda.current_stream(self.device).wait_event(done)
+        else:
+            self._halo_finish(hz)
+            self._halo_finish(self._halo_axis_start(dst, fields, 1))
+        if trace.ENABLED:
+            trace.pop()
+
     def exchange(self, buf: Optional[torch.Tensor] = None, fields=None):
         buf = self.snaps[self.cur] if buf is None else buf
         self._halo_finish(self._halo_start(buf, fields))
@@ -429,6 +470,12 @@ class Lattice:
                     self._launch_stage(si, dst, scratch, glob)
                     for r0, r1 in _runs(fields):
                         dst[r0:r1].copy_(scratch[r0:r1])
+                    self._halo_finish(self._halo_start(dst, fields))
+            elif self.overlap and self.slab.axis == 3:
+                if self.shape[1] > 2 * self.gy and self.shape[2] > 2 * self.gz:
+                    self._grid_overlapped(si, inp, dst, glob, fields)
+                else:
+                    self._launch_stage(si, inp, dst, glob)
                     self._halo_finish(self._halo_start(dst, fields))
             elif self.overlap and n > 2 * g:
                 if self.halo_mirror:

@@ -109,7 +109,7 @@ def decompose(gnx: int, gny: int, gnz: int, rank: int, size: int, halo: int = 1,
     py, pz = grid
     if py * pz != size:
         raise ValueError(f"grid {py}x{pz} does not match {size} ranks")
-    if pz == 1 or py == 1:              # degenerate grid: a slab along the split axis
+    if (pz == 1 or py == 1) and size > 1:   # degenerate grid: a slab along the split axis
         ax = 2 if py == 1 else 1
         nn = gnz if ax == 2 else gny
         lo, m = split(nn, size)[rank]

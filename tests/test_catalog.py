@@ -73,3 +73,34 @@ def test_dist_path_on_cpu_matches_loopback(name, mirror, monkeypatch):
     b = run(name, "cpu", steps=3, comm=LoopbackComm())
     assert a.overlap and a.halo_mirror == (mirror == "1")
     assert torch.equal(a.fields_interior(), b.fields_interior())
+
+
+MODELS_3D = [n for n in MODELS if registry.get(n).dims == 3]
+
+
+@pytest.mark.parametrize("name", MODELS_3D)
+def test_grid_path_on_cpu_matches_loopback(name, monkeypatch):
+    """the overlapped Y x Z grid step (four border slabs, two-phase z-then-y halo with the
+    edge ghosts, interior) with this rank as its own neighbour on both axes
+    (TCLB_GRID=1,1) equals the plain single-rank step, for every 3-D model"""
+    monkeypatch.setenv("TCLB_GRID", "1,1")
+    a = run(name, "cpu", steps=3, comm=LoopbackComm(exercise_dist_path=True))
+    monkeypatch.delenv("TCLB_GRID")
+    b = run(name, "cpu", steps=3, comm=LoopbackComm())
+    assert a.slab.axis == 3 and a.overlap and a.gy > 0 and a.gz > 0
+    assert torch.equal(a.fields_interior(), b.fields_interior())
+
+
+@pytest.mark.gpu
+@needs_gpu
+@pytest.mark.parametrize("name", MODELS_3D)
+def test_grid_path_on_gpu_matches_loopback(name, monkeypatch):
+    """GPU twin: the halo phases run on a side stream concurrently with the interior"""
+    monkeypatch.setenv("TCLB_GRID", "1,1")
+    a = run(name, "cuda", steps=3, comm=LoopbackComm(exercise_dist_path=True))
+    monkeypatch.delenv("TCLB_GRID")
+    b = run(name, "cuda", steps=3, comm=LoopbackComm())
+    assert a.slab.axis == 3 and a.overlap
+    fa, fb = a.fields_interior(), b.fields_interior()
+    scale = fb.abs().max().item() + 1e-300
+    assert torch.allclose(fa, fb, atol=1e-11 * scale, rtol=1e-11), (fa - fb).abs().max().item()
