@@ -6,8 +6,10 @@ applies the transposed local Jacobian — on the CPU (csrc/include/tclb/executor
 OpenMP) or on the GPU (csrc/include/tclb_ad/executor_ad_hip.hpp: windowed tangents,
 device fp64 atomics for the adjoint push), following the lattice's device.  This module
 drives it over actions (reverse stage order, in-place stages pass the adjoint of the
-fields they do not write through), folds ghost-plane contributions back to their owners,
-and runs unsteady adjoints with checkpointed recomputation of the primal trajectory.
+fields they do not write through), returns ghost-plane contributions to their owners
+(Lattice.reverse_halo: the periodic image on one rank, the neighbour rank over the
+communicator otherwise — every rank runs the adjoint of its own slab), and runs
+unsteady adjoints with checkpointed recomputation of the primal trajectory.
 
 Objective:  J = sum over the recorded iterations of the ``Objective`` global (the
 weighted sum of the model's globals, ``<G>InObj`` zonal weights), as in the reference.
@@ -33,8 +35,6 @@ class AdjointError(RuntimeError):
 
 class Adjoint:
     def __init__(self, lat, settings: Sequence[str] = (), zonal: Sequence[str] = ()):
-        if lat.comm.size > 1:
-            raise AdjointError("adjoint runs are single-rank")
         if lat.sdtype != torch.float64:
             raise AdjointError("adjoint needs double precision storage")
         self.lat = lat
@@ -54,23 +54,6 @@ class Adjoint:
         self._ctx_dev = torch.zeros(ctypes.sizeof(abi.AdCtx), dtype=torch.uint8, device=dev) if lat.is_gpu else None
 
     # ------------------------------------------------------------------ one action
-    def _fold_ghosts(self, a: torch.Tensor):
-        """adjoint contributions that landed in ghost planes belong to the periodic image"""
-        lat = self.lat
-        g = lat.g
-        if lat.slab.axis == 2 and lat.gz:
-            n = lat.shape[2]
-            a[:, g + n - g:g + n] += a[:, 0:g]
-            a[:, g:2 * g] += a[:, g + n:2 * g + n]
-            a[:, 0:g] = 0
-            a[:, g + n:2 * g + n] = 0
-        elif lat.slab.axis == 1 and lat.gy:
-            n = lat.shape[1]
-            a[:, :, g + n - g:g + n] += a[:, :, 0:g]
-            a[:, :, g:2 * g] += a[:, :, g + n:2 * g + n]
-            a[:, :, 0:g] = 0
-            a[:, :, g + n:2 * g + n] = 0
-
     def _ad_stage(self, si: int, inp: torch.Tensor, aout: torch.Tensor, obj_weight: float) -> torch.Tensor:
         lat = self.lat
         ain = torch.zeros_like(aout)
@@ -128,7 +111,7 @@ class Adjoint:
             self._ad_cover[si] = max(cover, c.reserved)
         if c.overflow:
             raise AdjointError(f"model {lat.model.name}: a node needed more than {self.lib.tangents} AD tangents")
-        self._fold_ghosts(ain)
+        lat.reverse_halo(ain)
         return ain
 
     def step_back(self, a_next: torch.Tensor, action: str = "Iteration", obj_weight: float = 1.0,
@@ -222,7 +205,10 @@ class Adjoint:
     def series_gradient(self, name: str, zone: Optional[str] = None) -> np.ndarray:
         lat = self.lat
         key = (lat.zsettings.index(name), lat.zone_index(zone or "DefaultZone"))
-        return self.series_grads.get(key, np.zeros(len(lat.zseries.get(key, [0.0])))).copy()
+        g = self.series_grads.get(key, np.zeros(len(lat.zseries.get(key, [0.0])))).copy()
+        if lat.comm.size > 1:
+            g = np.array([lat.comm.allreduce_scalar(float(v), "sum") for v in g])
+        return g
 
     def param_fields(self) -> List[int]:
         return [i for i, f in enumerate(self.lat.model.fields) if f.parameter]
@@ -246,7 +232,7 @@ class Adjoint:
         a = torch.zeros_like(self.lat.snaps[self.lat.cur])
         for _ in range(iterations):
             b = self.steady_step(a, action)
-            d = float((b - a).abs().max())
+            d = self.lat.comm.allreduce_scalar(float((b - a).abs().max()), "max") if tol else 0.0
             a = b
             if tol and d < tol:
                 break
@@ -263,8 +249,11 @@ class Adjoint:
         return self.a0[i, lat.gz:lat.gz + nz, lat.gy:lat.gy + ny, :nx].cpu().numpy().copy()
 
     def setting_gradient(self, name: str, zone: Optional[str] = None) -> float:
+        """d J / d setting, summed over the ranks (each accumulates its own nodes)"""
         lat = self.lat
         if name in lat.gsettings:
-            return float(self.gset[lat.gsettings.index(name)])
-        zi = lat.zone_index(zone or "DefaultZone")
-        return float(self.gzon[lat.zsettings.index(name) * lat.zvals.shape[1] + zi])
+            v = float(self.gset[lat.gsettings.index(name)])
+        else:
+            zi = lat.zone_index(zone or "DefaultZone")
+            v = float(self.gzon[lat.zsettings.index(name) * lat.zvals.shape[1] + zi])
+        return lat.comm.allreduce_scalar(v, "sum")

@@ -419,6 +419,43 @@ class Lattice:
         if trace.ENABLED:
             trace.pop()
 
+    def reverse_halo(self, a: torch.Tensor):
+        """adjoint of the halo exchange: contributions accumulated in the ghost planes of
+        an adjoint snapshot `a` are added to the planes of their owner (the neighbour
+        rank, or the periodic image on one rank) and the ghosts are cleared.  Phases in
+        the reverse order of the forward exchange (Y x Z grid: y rows over the
+        ghost-inclusive z extent, then z planes), so edge ghosts reach the diagonal
+        owner.  Reference: Iteration_Adj's reversed margin exchange and the atomic
+        adjoint push into the margins (src/Lattice.cu.Rt:542-613,
+        src/LatticeAccess.inc.cpp.Rt:349-361)."""
+        if self.g == 0:
+            return
+        axes = (1, 2) if self.slab.axis == 3 else (self.slab.axis,)
+        for axis in axes:
+            g = self.gz if axis == 2 else self.gy
+            n = self.shape[2] if axis == 2 else self.shape[1]
+            if g == 0:
+                continue
+            lo_ghost = self._axis_planes(a, 0, g, axis)              # owner: prev rank, its top planes
+            hi_ghost = self._axis_planes(a, n + g, n + 2 * g, axis)  # owner: next rank, its bottom planes
+            top = self._axis_planes(a, n, n + g, axis)
+            bottom = self._axis_planes(a, g, 2 * g, axis)
+            if not self.comm.distributed:
+                top += lo_ghost
+                bottom += hi_ghost
+            else:
+                send_up = hi_ghost.contiguous()
+                send_down = lo_ghost.contiguous()
+                recv_below = torch.empty_like(send_up)
+                recv_above = torch.empty_like(send_down)
+                nbr = self.slab.neighbours(axis) if self.slab.axis == 3 else None
+                h = self.comm.start_halo(send_up, send_down, recv_below, recv_above, nbr=nbr)
+                self.comm.wait_halo(h)
+                bottom += recv_below
+                top += recv_above
+            lo_ghost.zero_()
+            hi_ghost.zero_()
+
     def exchange(self, buf: Optional[torch.Tensor] = None, fields=None):
         buf = self.snaps[self.cur] if buf is None else buf
         self._halo_finish(self._halo_start(buf, fields))

@@ -133,3 +133,75 @@ def worker_checkpoint(rank, world, port, model, path, steps_before, steps_after,
                 f.write(str(parts[0][2]))
     dist.barrier()
     dist.destroy_process_group()
+
+
+def adjoint_case(model, comm=None, steps=10, grid=None, device="cpu"):
+    """unsteady adjoint of a small case: d3q19_adj pressure-driven duct through a porous
+    design block (z-slabs), d2q9_kuper two-stage stencil model (y-slabs) with a setting
+    gradient; returns (lattice, adjoint)"""
+    from tclb_amd.adjoint import Adjoint
+    from tclb_amd.lattice import Lattice
+    from tclb_amd.parallel.comm import LoopbackComm
+    comm = comm or LoopbackComm()
+    if model == "d3q19_adj":
+        nx, ny, nz = 10, 6, 8
+        lat = Lattice(model, (nx, ny, nz), comm=comm, grid=grid, device=torch.device(device))
+        m = lat.model
+        mrt = m.node_type("MRT").value
+        fl = np.full((lat.NZ, lat.NY, nx), mrt, dtype=np.uint32)
+        fl[:, :, 0] = m.node_type("WPressure").value | mrt
+        fl[:, :, nx - 1] = m.node_type("EPressure").value | mrt
+        fl[:, :, 7] |= m.node_type("Outlet").value
+        fl[:, :, 4:6] |= m.node_type("DesignSpace").value
+        lat.set_flags(fl)
+        for k, v in {"nu": 0.1, "InletDensity": 1.03, "FluxInObj": 1.0, "Theta": 1.0}.items():
+            lat.set_setting(k, v)
+        lat.init()
+        wi = m.field_index("w")
+        f = lat.fields_interior().clone()
+        oz = lat.slab.offset[2]
+        zz = torch.arange(lat.shape[2], dtype=f.dtype, device=f.device)[:, None, None] + oz
+        f[wi, :, :, 4:6] = (0.6 + 0.03 * zz).expand(-1, lat.shape[1], 2)
+        lat.set_fields_interior(f)
+        ad = Adjoint(lat, settings=["Theta"])
+    else:
+        nx, ny = 16, 12
+        lat = Lattice(model, (nx, ny, 1), comm=comm, device=torch.device(device))
+        m = lat.model
+        fl = np.full((lat.NZ, lat.NY, nx), m.node_type("MRT").value, dtype=np.uint32)
+        gy = (np.arange(lat.NY) + lat.slab.offset[1] - lat.gy) % ny
+        fl[:, gy == 0, :] = m.node_type("Wall").value
+        fl[:, gy == ny - 1, :] = m.node_type("Wall").value
+        lat.set_flags(fl)
+        for k, v in {"nu": 0.1666, "Magic": 0.005, "FAcc": 1.0, "Temperature": 0.65, "GravitationX": 1e-5,
+                     "Density": 1.0, "WallForceXInObj": 1.0}.items():
+            lat.set_setting(k, v)
+        lat.init()
+        ad = Adjoint(lat, settings=["GravitationX"])
+    ad.unsteady(steps)
+    return lat, ad
+
+
+def worker_adjoint(rank, world, port, model, out, grid=None):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from tclb_amd.parallel.comm import TorchDistComm
+    comm = TorchDistComm()
+    lat, ad = adjoint_case(model, comm, grid=grid)
+    nx, ny, nz = lat.shape
+    a = ad.a0[:, lat.gz:lat.gz + nz, lat.gy:lat.gy + ny, :nx].numpy()
+    name = "Theta" if model == "d3q19_adj" else "GravitationX"
+    sg = ad.setting_gradient(name)
+    parts = comm.gather_objects((lat.slab.offset, a))
+    if rank == 0:
+        gnx, gny, gnz = lat.gshape
+        full = np.zeros((lat.nf, gnz, gny, gnx))
+        for (ox, oy, oz), p in parts:
+            full[:, oz:oz + p.shape[1], oy:oy + p.shape[2], :] = p
+        np.save(out, full)
+        import json
+        with open(out + ".json", "w") as f:
+            json.dump({"J": ad.J, "grad": sg}, f)
+    dist.barrier()
+    dist.destroy_process_group()
