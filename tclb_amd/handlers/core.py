@@ -646,24 +646,51 @@ class Keep(Callback):
         return 0
 
 
+def _dedent(text: str) -> str:
+    import textwrap
+    lines = (text or "").split("\n")
+    while lines and not lines[0].strip():
+        lines.pop(0)
+    return textwrap.dedent("\n".join(lines)).rstrip()
+
+
 @register("RunPython")
 class RunPython(Callback):
-    """Embedded Python callback (reference RunR/RunPython, src/Handlers/cbRunR.cpp:687-845).
-    The element text is executed with ``solver``, ``lattice``, ``np``, ``torch`` in scope."""
+    """Embedded Python (reference RunR/RunPython, src/Handlers/cbRunR.cpp:687-845): the
+    element text runs in one namespace shared by every embedded block of the case, with
+    the reference's ``Solver`` object model (handlers/embed.py: Settings, Fields,
+    Parameters, Quantities, Globals, Actions, Geometry, Info) and ``np``; the raw
+    ``solver`` / ``lattice`` objects are there as well.  Without ``Iterations`` the block
+    runs once where it stands, otherwise every ``Iterations``; forces globals on the
+    last step (ITER_LASTGLOB) like the reference."""
 
     def init(self):
         super().init()
-        self.code = (self.node.text or "").strip()
-        if self.every_iter == 0:
-            pass
+        from ..solver import ITER_LASTGLOB
+        self.code = _dedent(self.node.text)
+        self.tag = f"<{self.node.tag} line {getattr(self.node, 'sourceline', '?')}>"
+        self._compiled = compile(self.code, self.tag, "exec") if self.code else None
+        self.old = self.solver.iter_type
+        self.solver.iter_type |= ITER_LASTGLOB
         return 0
 
     def do_it(self):
-        import torch
+        from .embed import namespace
         s = self.solver
-        env = {"solver": s, "lattice": s.lattice, "np": np, "torch": torch, "iteration": s.iter}
-        exec(compile(self.code, "<RunPython>", "exec"), env)
+        if self._compiled is None:
+            return 0
+        log.output(f"{s.iter:8d} it Executing {self.node.tag} code")
+        ns = namespace(s)
+        ns.update({"solver": s, "lattice": s.lattice, "iteration": s.iter})
+        try:
+            exec(self._compiled, ns)
+        except NameError as e:
+            raise HandlerError(f"{self.node.tag}: {e} (names available: Solver, np, solver, lattice)") from e
         return 0
+
+    def finish(self):
+        self.solver.iter_type = self.old
+        return super().finish()
 
 
 @register("Control")
@@ -991,11 +1018,13 @@ class RunR(Callback):
         if self.node.get("python", "false").lower() not in ("true", "1", "yes"):
             raise HandlerError("RunR: no embedded R interpreter in tclb_amd; "
                                "use <RunPython> (or RunR python=\"true\") with the equivalent Python code")
-        self.code = (self.node.text or "").strip()
-        return 0
+        return RunPython.init(self)
 
     def do_it(self):
         return RunPython.do_it(self)
+
+    def finish(self):
+        return RunPython.finish(self)
 
 
 @register("ESYSParticle")
