@@ -103,15 +103,30 @@ def infer_models(path: str, candidates=None, with_missing=False):
     return [n for k, _, n, _ in out if k == best]
 
 
-def capped_case(path: str, iters: int, outdir: str) -> str:
+OUTPUT_ELEMENTS = ("VTK", "TXT", "BIN", "HDF5", "Catalyst", "Log", "SaveCheckpoint", "SaveBinary", "Sample",
+                   "Failcheck", "DumpSettings")
+
+
+def capped_case(path: str, iters: int, outdir: str, no_output: bool = False) -> str:
+    """the case with every Solve/RunAction/OptSolve capped to `iters` (shorter ones kept),
+    Repeat to one pass, output redirected; no_output drops the output/check callbacks"""
     from tclb_amd.utils.xpath import load_case
     root = load_case(path)
     root.set("output", outdir.rstrip("/") + "/")
     for el in root.iter():
         if el.tag in ("Solve", "RunAction", "OptSolve") and "Iterations" in el.attrib:
-            el.set("Iterations", str(iters))
+            try:
+                n = min(iters, int(float(el.get("Iterations"))))
+            except ValueError:
+                n = iters
+            el.set("Iterations", str(n))
         if el.tag == "Repeat" and "Times" in el.attrib:
             el.set("Times", "1")
+    if no_output:
+        for parent in list(root.iter()):
+            for ch in list(parent):
+                if ch.tag in OUTPUT_ELEMENTS:
+                    parent.remove(ch)
     d = tempfile.mkdtemp(prefix="tclb_case_")
     tmp = os.path.join(d, os.path.basename(path))
     ET.ElementTree(root).write(tmp)
@@ -129,6 +144,7 @@ def main():
     ap.add_argument("--infer", action="store_true",
                     help="cases naming no model: pick the simplest catalog model that accepts every node type "
                          "and setting the case uses")
+    ap.add_argument("--no-output", action="store_true", help="drop VTK/Log/Failcheck/... (compute-only timing)")
     ap.add_argument("--cwd", default=None, help="working directory (default: the case's directory; the "
                                                  "reference resolves data paths like example/... from its root)")
     a = ap.parse_args()
@@ -154,14 +170,14 @@ def main():
             rec["status"] = "no model in header"
             print(json.dumps(rec), flush=True)
             continue
-        if re.search(r"<\s*(RunR|RunPython)\b", text):
-            # cases embedding R/Python code: the code in the case file is not executed here
-            rec["status"] = "skipped: embedded RunR/RunPython code"
+        if re.search(r"<\s*RunR\b", text) and not re.search(r"<\s*RunR[^>]*python=", text):
+            # cases embedding R code: no R interpreter (RunPython blocks do run)
+            rec["status"] = "skipped: embedded R code"
             print(json.dumps(rec), flush=True)
             continue
         out = os.path.join(a.out, os.path.splitext(os.path.basename(case))[0])
         os.makedirs(out, exist_ok=True)
-        tmp = capped_case(case, a.iters, out)
+        tmp = capped_case(case, a.iters, out, a.no_output)
         t0 = time.time()
         try:
             r = subprocess.run([sys.executable, "-m", "tclb_amd", model, tmp, "--device", a.device],
@@ -169,6 +185,8 @@ def main():
                                timeout=a.timeout, env={**os.environ, "PYTHONPATH": REPO})
             rec["status"] = "ok" if r.returncode == 0 else f"rc={r.returncode}"
             rec["tail"] = (r.stdout + r.stderr)[-600:]
+            # the solver's speed meter lines: "<iter> it <MLBUps> MLBUps <GB/s> GB/s"
+            rec["mlups"] = [float(v) for v in re.findall(r"it\s+([0-9.]+) MLBUps", r.stdout)]
         except subprocess.TimeoutExpired:
             rec["status"] = "timeout"
         finally:
