@@ -46,6 +46,12 @@ def main(argv=None):
     comm = init_distributed_from_env(a.device or "auto")
     s = Solver(a.model, root, conffile=a.config, device=a.device, precision=a.precision, comm=comm)
     s.run()
+    import torch.distributed as dist
+    if dist.is_available() and dist.is_initialized():
+        # leave together: a rank that exits while its peers are still in a collective
+        # makes their transport abort (gloo IoException)
+        dist.barrier()
+        dist.destroy_process_group()
     return 0
 
 

@@ -796,7 +796,7 @@ class Lattice:
         L.reserved1 = max(1, self.iter - self.average_start)
         L.stream = self._stream()
         if self.particles is not None:   # quantities may look at particles (e.g. Checks)
-            self.particles.pre_stage(self)
+            self.particles.attach_for_quantity(self)
         try:
             self.lib.quantity(L, self.prec)
         finally:

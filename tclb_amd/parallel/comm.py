@@ -41,6 +41,14 @@ class Comm:
     def gather_objects(self, obj) -> List:
         return [obj]
 
+    def scatter_objects(self, objs: Optional[List], src: int = 0):
+        """objs[r] (given on src) -> rank r"""
+        return objs[0]
+
+    def gather_to_root(self, obj, dst: int = 0) -> Optional[List]:
+        """every rank's obj, on dst only (None elsewhere)"""
+        return [obj]
+
     def start_halo(self, send_up: Optional[torch.Tensor], send_down: Optional[torch.Tensor],
                    recv_below: Optional[torch.Tensor], recv_above: Optional[torch.Tensor], nbr=None):
         """send_up -> next, send_down -> prev, recv_below <- prev, recv_above <- next;
@@ -118,6 +126,16 @@ class TorchDistComm(Comm):
     def gather_objects(self, obj) -> List:
         out = [None] * self.size
         self.dist.all_gather_object(out, obj, group=self.group)
+        return out
+
+    def scatter_objects(self, objs, src: int = 0):
+        out = [None]
+        self.dist.scatter_object_list(out, objs if self.rank == src else None, src=self._g(src), group=self.group)
+        return out[0]
+
+    def gather_to_root(self, obj, dst: int = 0):
+        out = [None] * self.size if self.rank == dst else None
+        self.dist.gather_object(obj, out, dst=self._g(dst), group=self.group)
         return out
 
     def start_halo(self, send_up, send_down, recv_below, recv_above, nbr=None):

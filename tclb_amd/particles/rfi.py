@@ -17,8 +17,12 @@ stream socket between rank 0 of the lattice job and the integrator:
     calculator -> STOP         (the lattice run ended; the integrator exits)
 
 FORCES carries integrate = 0 after a particle stage of the Init action (no time step,
-as the in-process SIMPLEPART does not step in Init) and 1 otherwise.  Other ranks get
-the particles by broadcast; forces are all-reduced before rank 0 sends them.
+as the in-process SIMPLEPART does not step in Init) and 1 otherwise.
+
+Multi-rank: like the reference RFI, each rank receives only the particles that can act
+on its box (sphere of radius r + 2, the kernels' cut-off, overlapping the rank's nodes;
+src/RemoteForceInterface.h:52-178): rank 0 scatters the per-rank subsets with their
+global indices and gathers the per-rank partial forces back, summing them in rank order.
 """
 from __future__ import annotations
 
@@ -107,6 +111,18 @@ def unpack_forces(p: bytes) -> Tuple[bool, np.ndarray]:
     return bool(integrate), np.frombuffer(p, dtype="<f8", count=n * 6, offset=16).reshape(n, 6).copy()
 
 
+def box_subset(rec: np.ndarray, offset, shape) -> np.ndarray:
+    """indices of the particle records whose influence sphere (radius r + 2) overlaps the
+    node box [offset, offset + shape) in every dimension"""
+    if len(rec) == 0:
+        return np.zeros(0, dtype=np.int64)
+    c, reach = rec[:, 0:3], rec[:, 9:10] + 2.0
+    lo = np.asarray(offset, float)[None]
+    hi = lo + np.asarray(shape, float)[None] - 1.0
+    ok = ((c + reach) >= lo) & ((c - reach) <= hi)
+    return np.nonzero(ok.all(1))[0]
+
+
 class RemoteParticles(ParticleSystem):
     """The lattice side (ForceCalculator).  Rank 0 listens on ``address`` (port 0: any
     free port, see ``.address``) and accepts one integrator; ``accept()`` completes the
@@ -123,6 +139,10 @@ class RemoteParticles(ParticleSystem):
         self._pending = False
         self.exchanges = 0
         self._srv = None
+        self._boxes = None            # (offset, shape) of every rank
+        self._idx = np.zeros(0, dtype=np.int64)
+        self._full = np.zeros((0, 6))  # forces/torques of all particles (rank 0)
+        self.n_total = 0
         if self._root:
             host, port = parse_address(address)
             self._srv = socket.create_server((host, port))
@@ -150,32 +170,59 @@ class RemoteParticles(ParticleSystem):
                                               "box": self.box}).encode())
         return self
 
-    def _bcast(self, obj):
-        return self.comm.bcast_object(obj) if self.comm is not None and self.comm.size > 1 else obj
+    @property
+    def _multi(self) -> bool:
+        return self.comm is not None and self.comm.distributed and self.comm.size > 1
+
+    @property
+    def forces_all(self) -> np.ndarray:
+        """(n, 6) forces and torques of every particle of the last exchange (rank 0)"""
+        return self._full
 
     def _send_forces(self, integrate: bool):
         if self._root:
-            self.chan.send(FORCES, pack_forces(self.force, self.torque, integrate))
+            self.chan.send(FORCES, pack_forces(self._full[:, 0:3], self._full[:, 3:6], integrate))
         self._pending = False
 
     # -- lattice hooks --------------------------------------------------------------
     def pre_stage(self, lat):
         if self._pending:            # the last particle stage was not followed by a step (Init)
             self._send_forces(False)
-        rec = unpack_particles(self.chan.expect(PARTICLES)) if self._root else None
-        rec = self._bcast(rec)
-        self.x, self.v, self.omega = rec[:, 0:3].copy(), rec[:, 3:6].copy(), rec[:, 6:9].copy()
-        self.r = rec[:, 9].copy()
-        n = len(self.r)
+        if self._boxes is None:
+            box = (tuple(lat.slab.offset), tuple(lat.shape))
+            self._boxes = self.comm.gather_objects(box) if self._multi else [box]
+        parts = None
+        if self._root:
+            rec = unpack_particles(self.chan.expect(PARTICLES))
+            self.n_total = len(rec)
+            parts = []
+            for off, shp in self._boxes:
+                idx = box_subset(rec, off, shp)
+                parts.append((idx, rec[idx]))
+        idx, sub = self.comm.scatter_objects(parts) if self._multi else parts[0]
+        self._idx = idx
+        self.x, self.v, self.omega = sub[:, 0:3].copy(), sub[:, 3:6].copy(), sub[:, 6:9].copy()
+        self.r = sub[:, 9].copy()
+        n = len(sub)
         self.m = np.zeros(n)
         self.fixed = np.zeros(n, dtype=bool)
         self.force = np.zeros((n, 3))
         self.torque = np.zeros((n, 3))
         self.exchanges += 1
-        super().pre_stage(lat)
+        ParticleSystem.pre_stage(self, lat)
 
     def post_stage(self, lat):
-        super().post_stage(lat)
+        # partial forces of this rank's subset; summed on rank 0 (no all-reduce of the
+        # whole particle set)
+        self._host_stale |= {"force", "torque"}
+        self.detach(lat)
+        f = np.concatenate([self.force, self.torque], axis=1) if len(self._idx) else np.zeros((0, 6))
+        parts = self.comm.gather_to_root((self._idx, f)) if self._multi else [(self._idx, f)]
+        if self._root:
+            full = np.zeros((self.n_total, 6))
+            for idx, fr in parts:
+                full[idx] += fr
+            self._full = full
         self._pending = True
 
     def step(self, lat):

@@ -1,4 +1,17 @@
-"""Particle system + built-in rigid-sphere integrator (reference simplepart.cpp)."""
+"""Particle system + built-in rigid-sphere integrator (reference simplepart.cpp,
+src/RemoteForceInterface.*, src/SolidGrid.h).
+
+Device-resident design: once attached to a lattice the particle records live on the
+lattice's device — ``P`` (n, 10: position, velocity, angular velocity, radius), the
+force/moment accumulator ``acc`` (n, 6) that the particle stage kernels add into, the
+uniform-grid solid container, and (SimplePart) the rigid-body integration.  A time step
+therefore issues only device work: zero ``acc`` -> particle stage kernel -> all-reduce of
+``acc`` over the ranks (RCCL: asynchronous, no host round trip) -> integration kernel.
+The host copies (``x``, ``v``, ``omega``, ``force``, ``torque``) are refreshed lazily,
+only when something reads them (a particle log, the socket RFI, a test): the reference's
+per-iteration MPI exchange with the integrator is replaced by no synchronisation at all
+on the steps without callbacks.
+"""
 from __future__ import annotations
 
 import math
@@ -9,74 +22,157 @@ import numpy as np
 import torch
 
 PART_STRIDE = 10
+_HOST = ("x", "v", "omega", "r", "m", "force", "torque", "fixed")
+
+
+def _host_prop(name):
+    def get(self):
+        if name in self._host_stale:
+            self._pull()
+        return self._h[name]
+
+    def set_(self, value):
+        if self._host_stale:
+            self._pull()
+        self._h[name] = value
+        self._dev_stale = True
+    return property(get, set_)
 
 
 class ParticleSystem:
     """Particles in lattice units (positions in node coordinates)."""
 
+    x = _host_prop("x")
+    v = _host_prop("v")
+    omega = _host_prop("omega")
+    r = _host_prop("r")
+    m = _host_prop("m")
+    force = _host_prop("force")
+    torque = _host_prop("torque")
+    fixed = _host_prop("fixed")
+
     def __init__(self, n: int = 0):
-        self.x = np.zeros((n, 3))
-        self.v = np.zeros((n, 3))
-        self.omega = np.zeros((n, 3))
-        self.r = np.zeros(n)
-        self.m = np.zeros(n)
-        self.force = np.zeros((n, 3))
-        self.torque = np.zeros((n, 3))
-        self.fixed = np.zeros(n, dtype=bool)
-        self._dev = None
-        self._acc = None
-        self._grid = None
-        self.grid_min = 16          # particles; below this every node scans the full list
+        self._h = {"x": np.zeros((n, 3)), "v": np.zeros((n, 3)), "omega": np.zeros((n, 3)), "r": np.zeros(n),
+                   "m": np.zeros(n), "force": np.zeros((n, 3)), "torque": np.zeros((n, 3)),
+                   "fixed": np.zeros(n, dtype=bool)}
+        self._host_stale = set()      # host arrays older than the device copy
+        self._dev_stale = True        # device copy older than the host arrays
+        self._d = None                # device tensors (P, acc, qacc, m, free, grid)
+        self._dev_key = None
+        self.grid_min = 16            # particles; below this every node scans the full list
 
     @property
     def n(self) -> int:
-        return len(self.r)
+        return len(self._h["r"])
 
     def add(self, x, r, v=(0, 0, 0), omega=(0, 0, 0), m=None, fixed=False):
-        self.x = np.vstack([self.x, np.asarray(x, float)[None]])
-        self.v = np.vstack([self.v, np.asarray(v, float)[None]])
-        self.omega = np.vstack([self.omega, np.asarray(omega, float)[None]])
-        self.r = np.append(self.r, float(r))
-        self.m = np.append(self.m, float(m) if m else 4.0 / 3.0 * math.pi * r ** 3)
-        self.force = np.vstack([self.force, np.zeros((1, 3))])
-        self.torque = np.vstack([self.torque, np.zeros((1, 3))])
-        self.fixed = np.append(self.fixed, bool(fixed))
+        if self._host_stale:
+            self._pull()
+        h = self._h
+        h["x"] = np.vstack([h["x"], np.asarray(x, float)[None]])
+        h["v"] = np.vstack([h["v"], np.asarray(v, float)[None]])
+        h["omega"] = np.vstack([h["omega"], np.asarray(omega, float)[None]])
+        h["r"] = np.append(h["r"], float(r))
+        h["m"] = np.append(h["m"], float(m) if m else 4.0 / 3.0 * math.pi * r ** 3)
+        h["force"] = np.vstack([h["force"], np.zeros((1, 3))])
+        h["torque"] = np.vstack([h["torque"], np.zeros((1, 3))])
+        h["fixed"] = np.append(h["fixed"], bool(fixed))
+        self._dev_stale = True
 
-    # -- lattice hooks --------------------------------------------------------------
-    def pre_stage(self, lat):
-        rec = np.zeros((max(1, self.n), PART_STRIDE))
-        if self.n:
-            rec[:self.n, 0:3] = self.x
-            rec[:self.n, 3:6] = self.v
-            rec[:self.n, 6:9] = self.omega
-            rec[:self.n, 9] = self.r
-        self._dev = torch.as_tensor(rec).to(lat.device)
-        self._acc = torch.zeros((max(1, self.n), 6), dtype=torch.float64, device=lat.device)
+    # -- host <-> device ------------------------------------------------------------
+    def _push(self, lat):
+        """upload the host arrays (after a host-side change or a device change)"""
+        h, n, dev = self._h, self.n, lat.device
+        rec = np.zeros((max(1, n), PART_STRIDE))
+        if n:
+            rec[:n, 0:3], rec[:n, 3:6], rec[:n, 6:9], rec[:n, 9] = h["x"], h["v"], h["omega"], h["r"]
+        acc = np.zeros((max(1, n), 6))
+        if n:
+            acc[:n, 0:3], acc[:n, 3:6] = h["force"], h["torque"]
+        d = {"P": torch.as_tensor(rec).to(dev), "acc": torch.as_tensor(acc).to(dev),
+             "qacc": torch.zeros((max(1, n), 6), dtype=torch.float64, device=dev),
+             "m": torch.as_tensor(np.where(h["m"] > 0, h["m"], 1.0) if n else np.ones(1)).to(dev),
+             "free": torch.as_tensor(~h["fixed"] if n else np.zeros(1, dtype=bool)).to(dev)}
+        d["grid"], d["cell"] = None, 1
+        if n >= self.grid_min:
+            d["cell"] = int(np.ceil(h["r"].max() + 2.0))
+            gx, gy, gz = (-(-s // d["cell"]) for s in lat.gshape)
+            d["ncell"] = gx * gy * gz
+            d["grid"] = torch.zeros(9 + d["ncell"] + n, dtype=torch.int32, device=dev)
+            d["grid"][:4] = torch.tensor([gx, gy, gz, d["cell"]], dtype=torch.int32)
+            d["gdim"] = (gx, gy, gz)
+        self._d = d
+        self._dev_key = (str(dev), n)
+        self._dev_stale = False
+        self._host_stale = set()
+
+    def _pull(self):
+        """refresh the host arrays from the device (one synchronising copy)"""
+        if self._d is None or not self._host_stale:
+            self._host_stale = set()
+            return
+        n = self.n
+        P = self._d["P"][:n].cpu().numpy()
+        acc = self._d["acc"][:n].cpu().numpy()
+        h = self._h
+        h["x"], h["v"], h["omega"] = P[:, 0:3].copy(), P[:, 3:6].copy(), P[:, 6:9].copy()
+        h["force"], h["torque"] = acc[:, 0:3].copy(), acc[:, 3:6].copy()
+        self._host_stale = set()
+
+    def _ensure(self, lat):
+        if self._dev_stale or self._d is None or self._dev_key != (str(lat.device), self.n):
+            self._push(lat)
+
+    def _build_grid(self):
+        """uniform-grid solid container on the device, the layout of tclb_solid_grid
+        (csrc/runtime/host.cpp): header gx gy gz cell, cell starts, particle ids sorted by
+        cell (stable: ascending id inside a cell); no host round trip"""
+        d, n = self._d, self.n
+        gx, gy, gz = d["gdim"]
+        c = torch.floor(d["P"][:n, 0:3] / d["cell"]).to(torch.int64)
+        c[:, 0].clamp_(0, gx - 1)
+        c[:, 1].clamp_(0, gy - 1)
+        c[:, 2].clamp_(0, gz - 1)
+        cid = (c[:, 2] * gy + c[:, 1]) * gx + c[:, 0]
+        cnt = torch.zeros(d["ncell"] + 1, dtype=torch.int64, device=cid.device)
+        cnt.scatter_add_(0, cid + 1, torch.ones_like(cid))
+        g = d["grid"]
+        g[8:9 + d["ncell"]] = torch.cumsum(cnt, 0).to(torch.int32)
+        g[9 + d["ncell"]:] = torch.sort(cid, stable=True).indices.to(torch.int32)
+
+    def _attach(self, lat, acc):
+        d = self._d
         L = lat._L
-        L.ext[2] = self._dev.data_ptr()
-        L.ext[3] = self._acc.data_ptr()
+        L.ext[2] = d["P"].data_ptr()
+        L.ext[3] = acc.data_ptr()
         L.next[2] = self.n
-        # solid container: uniform grid (reference default SolidGrid) once the linear scan
-        # over all particles per node stops being cheap
-        self._grid = None
-        if self.n >= self.grid_min:
-            from ..ops.host import solid_grid
-            cell = int(np.ceil(self.r[:self.n].max() + 2.0)) if self.n else 1
-            g = solid_grid(rec[:self.n], lat.gshape, cell)
-            self._grid = torch.as_tensor(g).to(lat.device)
-            L.ext[4] = self._grid.data_ptr()
-            L.next[4] = self._grid.numel()
+        if d["grid"] is not None:
+            self._build_grid()
+            L.ext[4] = d["grid"].data_ptr()
+            L.next[4] = d["grid"].numel()
         else:
             L.ext[4] = None
             L.next[4] = 0
 
+    # -- lattice hooks --------------------------------------------------------------
+    def pre_stage(self, lat):
+        """before a particle stage: zero the accumulator, hand the records to the launch"""
+        self._ensure(lat)
+        self._d["acc"].zero_()
+        self._attach(lat, self._d["acc"])
+
+    def attach_for_quantity(self, lat):
+        """before a quantity launch (quantities may look at particles): the current
+        records, and a scratch accumulator so the stage's forces are not disturbed"""
+        self._ensure(lat)
+        self._d["qacc"].zero_()
+        self._attach(lat, self._d["qacc"])
+
     def post_stage(self, lat):
-        acc = self._acc
+        acc = self._d["acc"]
         if lat.comm.distributed and lat.comm.size > 1:
-            acc = lat.comm.allreduce_globals(acc.reshape(-1).clone(), acc.numel()).reshape(acc.shape)
-        a = acc.cpu().numpy()[:self.n]
-        self.force = a[:, 0:3].copy()
-        self.torque = a[:, 3:6].copy()
+            acc.copy_(lat.comm.allreduce_globals(acc.reshape(-1).clone(), acc.numel()).reshape(acc.shape))
+        self._host_stale |= {"force", "torque"}
         self.detach(lat)
 
     def detach(self, lat):
@@ -90,8 +186,9 @@ class ParticleSystem:
 
 
 def integrate_rigid(x, v, omega, r, m, fixed, force, torque, acc, periodic, period):
-    """one explicit step of free rigid spheres (reference simplepart.cpp), in place; shared
-    by the in-process SimplePart and the remote integrator tools/rfi_simplepart.py"""
+    """one explicit step of free rigid spheres (reference simplepart.cpp), in place, on
+    host arrays; used by the stand-alone integrator tools/rfi_simplepart.py.  The
+    in-process SimplePart runs the same update on the device (SimplePart._integrate)."""
     for i in range(len(r)):
         if fixed[i]:
             continue
@@ -106,7 +203,7 @@ def integrate_rigid(x, v, omega, r, m, fixed, force, torque, acc, periodic, peri
 
 class SimplePart(ParticleSystem):
     """Built-in rigid spheres (reference simplepart: explicit integration, optional
-    periodicity, constant acceleration, logging)."""
+    periodicity, constant acceleration, logging), integrated on the lattice's device."""
 
     def __init__(self):
         super().__init__(0)
@@ -119,10 +216,31 @@ class SimplePart(ParticleSystem):
         self.logged: List[int] = []
         self.iteration = 0
 
+    def _integrate(self):
+        """the update of integrate_rigid, vectorised over the particles on the device:
+        v += F/m + a; x += v; omega += T/I (I = 2/5 m r^2); periodic wrap"""
+        d, n = self._d, self.n
+        if n == 0:
+            return
+        P, acc = d["P"][:n], d["acc"][:n]
+        x, v, w, r = P[:, 0:3], P[:, 3:6], P[:, 6:9], P[:, 9]
+        m = d["m"][:n]
+        free = d["free"][:n, None]
+        a = torch.as_tensor(self.acc, dtype=torch.float64, device=P.device)
+        nv = v + (acc[:, 0:3] / m[:, None] + a)
+        nx = x + nv
+        nw = w + acc[:, 3:6] / (0.4 * m * r ** 2)[:, None]
+        for k in range(3):
+            if self.periodic[k] and self.period[k] > 0:
+                nx[:, k] = torch.remainder(nx[:, k], float(self.period[k]))
+        v.copy_(torch.where(free, nv, v))
+        x.copy_(torch.where(free, nx, x))
+        w.copy_(torch.where(free, nw, w))
+        self._host_stale |= {"x", "v", "omega"}
+
     def step(self, lat):
         self.iteration += 1
-        integrate_rigid(self.x, self.v, self.omega, self.r, self.m, self.fixed, self.force, self.torque, self.acc,
-                        self.periodic, self.period)
+        self._integrate()
         if self.log_path and self.iteration % self.log_every == 0 and lat.comm.rank == 0:
             self._log()
 

@@ -44,7 +44,10 @@ def _run(workdir, model, case, nproc):
                "--master-addr", "127.0.0.1", "--master-port", str(_port()), "-m", "tclb_amd", model, case,
                "--device", "cpu"]
     r = subprocess.run(cmd, cwd=workdir, env=env, capture_output=True, text=True, timeout=600)
-    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    if r.returncode != 0:
+        err = r.stderr
+        k = max(err.find("Traceback"), err.find("terminate called"))
+        raise AssertionError(f"rc={r.returncode}\n" + r.stdout[-1500:] + (err[k:k + 4000] if k >= 0 else err[-4000:]))
 
 
 def _case_dir(tmp_path, tag, src):
@@ -147,3 +150,43 @@ def test_particle_xml_ranks_match_single(tmp_path):
     assert np.abs(forces).max() > 0
     np.testing.assert_allclose(lb, la, rtol=1e-12, atol=1e-12 * np.abs(forces).max())
     assert la[-1, 1] > 14.3 + 0.05                    # the particle moved in x
+
+
+RFI_CASE = """<?xml version="1.0"?>
+<CLBConfig version="2.0" output="output/">
+  <Geometry nx="32" ny="24" nz="24"><MRT><Box/></MRT></Geometry>
+  <Model><Param name="Viscosity" value="0.1"/></Model>
+  <RemoteForceInterface integrator="simplepart_remote" spawn="{spawn}"/>
+  <Solve Iterations="8"/>
+</CLBConfig>"""
+
+
+def test_socket_rfi_two_ranks_match_single(tmp_path):
+    """the socket RFI on 2 ranks (rank 0 scatters each rank the particles of its box and
+    sums the partial forces) drives the external integrator exactly like 1 rank: same
+    trajectory in the integrator log to 1e-12; the particle near z = 0 reaches only the
+    lower slab"""
+    import json as _json
+    tool = os.path.join(ROOT, "tools", "rfi_simplepart.py")
+    parts = [{"x": [16.0, 12.0, 11.5], "r": 4.0, "v": [0.02, 0.0, 0.01], "m": 300.0},
+             {"x": [8.0, 6.0, 3.0], "r": 2.0, "v": [0.0, 0.01, 0.0], "m": 40.0}]
+    logs = []
+    for tag, n in (("one", 1), ("two", 2)):
+        d = tmp_path / tag
+        d.mkdir()
+        (d / "parts.json").write_text(_json.dumps({"particles": parts}))
+        spawn = f"{sys.executable} {tool} --address {{address}} --config parts.json --log log.csv"
+        (d / "rfi.xml").write_text(RFI_CASE.format(spawn=spawn))
+        _run(d, "auto_d3q19_part", "rfi.xml", n)
+        logs.append(np.loadtxt(d / "log.csv", delimiter=",", skiprows=1))
+    a, b = logs
+    assert a.shape == b.shape and a.shape[0] == 8
+    # the per-node force sums go through atomics: components that cancel to ~1e-15 carry
+    # the order noise of O(1) sums
+    np.testing.assert_allclose(b, a, rtol=1e-12, atol=1e-12 * np.abs(a[:, 7:10]).max())
+    from tclb_amd.particles.rfi import box_subset
+    rec = np.zeros((2, 10))
+    rec[:, 0:3] = [p["x"] for p in parts]
+    rec[:, 9] = [p["r"] for p in parts]
+    lower, upper = box_subset(rec, (0, 0, 0), (32, 24, 12)), box_subset(rec, (0, 0, 12), (32, 24, 12))
+    assert lower.tolist() == [0, 1] and upper.tolist() == [0]

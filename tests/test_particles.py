@@ -127,3 +127,35 @@ def test_d2q9_particle_velocity_coupling(name):
         assert sp.force[0, 0] < 0 and abs(sp.force[0, 1]) < 1e-3 * abs(sp.force[0, 0])
         assert lat.quantity("Checks").numpy()[0][0][12, cx] >= 1
     assert u[12, (cx + 8) % nx] > 1e-4                # fluid ahead is pushed along
+
+
+def _grid_case(device):
+    import torch as _t
+    from tclb_amd.lattice import Lattice as _L
+    from tclb_amd.ops.host import solid_grid
+    from tclb_amd.particles import SimplePart as _SP
+    rng = np.random.default_rng(5)
+    lat = _L("auto_d3q19_part", (40, 30, 20), device=_t.device(device))
+    sp = _SP()
+    for _ in range(40):
+        sp.add(rng.uniform([-3, 0, 0], [43, 30, 20]), rng.uniform(1.0, 3.0))
+    sp.pre_stage(lat)
+    dev = sp._d["grid"].cpu().numpy()
+    rec = np.zeros((sp.n, 10))
+    rec[:, 0:3], rec[:, 9] = sp.x, sp.r
+    host = solid_grid(rec, lat.gshape, int(np.ceil(sp.r.max() + 2.0)))
+    return dev, host
+
+
+def test_device_solid_grid_equals_host_container():
+    """the uniform-grid container built on the device (particles/system.py) equals the
+    native host container (csrc/runtime/host.cpp tclb_solid_grid) entry for entry"""
+    dev, host = _grid_case("cpu")
+    assert np.array_equal(dev, host)
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not torch.cuda.is_available(), reason="no GPU")
+def test_device_solid_grid_equals_host_container_gpu():
+    dev, host = _grid_case("cuda")
+    assert np.array_equal(dev, host)

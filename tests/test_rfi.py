@@ -78,7 +78,7 @@ def test_remote_integrator_matches_in_process(tmp_path):
     rp.close()
     assert proc.wait(60) == 0
     assert torch.allclose(a.fields_interior(), b.fields_interior(), rtol=0, atol=1e-13)
-    np.testing.assert_allclose(sp.force, rp.force, rtol=1e-10, atol=1e-14)
+    np.testing.assert_allclose(sp.force, rp.forces_all[:, 0:3], rtol=1e-10, atol=1e-14)
     rows = open(tmp_path / "log.csv").read().splitlines()
     assert len(rows) == steps + 1                    # header + one row per integrated step
     x_remote = [float(v) for v in rows[-1].split(",")[1:4]]
