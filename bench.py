@@ -60,6 +60,8 @@ def main():
     ap.add_argument("--block", default="0,0")
     ap.add_argument("--no-overlap", action="store_true")
     ap.add_argument("--cpu", action="store_true")
+    ap.add_argument("--glob-every-step", action="store_true",
+                    help="globals on every step (a <Log Iterations=\"1\">-style run), not only the last")
     ap.add_argument("--loopback-dist", action="store_true",
                     help="1 rank through the multi-rank path (border/interior split + pack/unpack)")
     a = ap.parse_args()
@@ -96,7 +98,11 @@ def main():
     lat.iterate(a.warmup, glob_last=False)
     sync()
     t0 = time.perf_counter()
-    lat.iterate(a.steps, glob_last=True)
+    if a.glob_every_step:
+        for _ in range(a.steps):
+            lat.iterate(1, glob_last=True)
+    else:
+        lat.iterate(a.steps, glob_last=True)
     sync()
     dt = time.perf_counter() - t0
     dt = comm.allreduce_scalar(dt, "max")

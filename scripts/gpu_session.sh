@@ -50,9 +50,10 @@ adwin)
     step "adjoint bench 128 window ${v:-w3}" 300 $O/bench_adjoint_128_${v:-w3}.json env TCLB_AD_VARIANT=$v python tools/bench_adjoint.py --size 128 --steps 80
   done ;;
 refcases)
-  step "ThermocapillaryFlow x20, 200 its" 900 $O/examples_thermocapillary_gpu.jsonl python tools/run_examples.py --device cuda --iters 200 --out /tmp/tclb_ex $R/_refcases/ThermocapillaryFlow/*.xml
-  step "annular Taylor bubble 3000 its, output as written" 600 $O/annular_output.jsonl python tools/run_examples.py --device cuda --iters 3000 --out /tmp/tclb_ex $R/_refcases/annular/annularTaylorBubble_DasC.xml
-  step "annular Taylor bubble 3000 its, no output" 600 $O/annular_nooutput.jsonl python tools/run_examples.py --device cuda --iters 3000 --no-output --out /tmp/tclb_ex2 $R/_refcases/annular/annularTaylorBubble_DasC.xml ;;
+  step "ThermocapillaryFlow x20, 200 its" 900 $O/examples_thermocapillary_gpu.jsonl python tools/run_examples.py --device cuda --iters 200 --out /tmp/tclb_ex $R/_refcases/ThermocapillaryFlow/*.xml ;&
+annular)
+  step "annular Taylor bubble 3000 its, output as written" 600 $O/annular_output.jsonl python tools/run_examples.py --device cuda --iters 3000 --out /tmp/tclb_ex $R/_refcases/d3q27_pf_velocity/annularTaylorBubble_DasC.xml
+  step "annular Taylor bubble 3000 its, no output" 600 $O/annular_nooutput.jsonl python tools/run_examples.py --device cuda --iters 3000 --no-output --out /tmp/tclb_ex2 $R/_refcases/d3q27_pf_velocity/annularTaylorBubble_DasC.xml ;;
 smoke) step "smoke" 300 $O/smoke.log python -c "import __graft_entry__ as g; g.smoke()" ;;
 bench1) step "bench fp64" 300 $O/bench_fp64.json python bench.py ;;
 esac; done

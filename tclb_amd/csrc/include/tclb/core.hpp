@@ -22,8 +22,15 @@
 
 #define TCLB_UNROLL _Pragma("unroll")
 #define TCLB_MIRROR_FIELDS 128   // halo-mirror slot table size (Launch.mslot); models have <= 109 fields
+// Globals accumulate into TCLB_GSLOTS slots of gstride(NG) doubles (one or more 128-B
+// lines each): block b adds into slot b % TCLB_GSLOTS, so the per-block atomics of a
+// launch spread over 64 addresses per global instead of queueing on one (the host sums
+// and max-reduces the slots, lattice.py _reduce_globals; ops/abi.py GSLOTS).
+#define TCLB_GSLOTS 64
 
 namespace tclb {
+
+TCLB_FN constexpr int gstride(int ng) { return (ng + 15) / 16 * 16; }
 
 typedef uint32_t flag_t;  // node type word (reference: flag_t 16/32 bit, src/conf.R:620-628)
 

@@ -42,7 +42,11 @@ __device__ __forceinline__ void atomic_max_double(double* addr, double v) {
   }
 }
 
-// Reduce per-thread accumulators g[NG] of a block and add into dst (device, double).
+// Reduce per-thread accumulators g[NG] of a block and add into slot (block % TCLB_GSLOTS)
+// of dst (device, double; core.hpp TCLB_GSLOTS).  One atomic per block and global, but
+// the blocks of a launch spread over TCLB_GSLOTS addresses: with every block adding into
+// the same 8 bytes the L2 serialises ~10^5-10^6 atomics per global and launch
+// (profiles/README.md r03: the GLOB instantiations ran +25-46 % over the plain ones).
 template <int NG, int NSUM, class R>
 __device__ __forceinline__ void block_globals(R* g, double* dst) {
   __shared__ double part[NG][16];
@@ -56,6 +60,8 @@ __device__ __forceinline__ void block_globals(R* g, double* dst) {
   }
   __syncthreads();
   if (tid < NG) {
+    const unsigned b = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+    dst += (b % TCLB_GSLOTS) * (unsigned)gstride(NG);
     double acc = part[tid][0];
     for (int w = 1; w < nw; w++) acc = tid < NSUM ? acc + part[tid][w] : (acc > part[tid][w] ? acc : part[tid][w]);
     if (tid < NSUM) {

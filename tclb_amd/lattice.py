@@ -136,7 +136,10 @@ class Lattice:
         self._settings_dirty = True
         self.settings_t = torch.zeros(self.svals.shape, dtype=torch.float64, device=self.device)
         self.zonal_t = torch.zeros(self.zvals.size, dtype=torch.float64, device=self.device)
-        self.globals_t = torch.zeros(max(1, len(m.globals_)), dtype=torch.float64, device=self.device)
+        # globals accumulator: GSLOTS slots of gstride(NG) doubles (core.hpp TCLB_GSLOTS);
+        # the GPU blocks add into slot (block % GSLOTS), the CPU executor into slot 0
+        self._gstride = abi.gstride(max(1, len(m.globals_)))
+        self.globals_t = torch.zeros(abi.GSLOTS * self._gstride, dtype=torch.float64, device=self.device)
         self.globals: Dict[str, float] = {g.name: 0.0 for g in m.globals_}
         self.iter = 0
         self.block = block
@@ -544,9 +547,18 @@ class Lattice:
                 self.snaps[0].shape, self.snaps[0].stride())
         return self._scratch
 
+    def globals_vector(self) -> torch.Tensor:
+        """the NG globals of this rank: SUM globals summed and MAX globals max-reduced
+        over the accumulator slots"""
+        ng, ns = len(self.model.globals_), self.model.n_sum_globals
+        slots = self.globals_t.view(abi.GSLOTS, self._gstride)[:, :ng]
+        if ns == ng:
+            return slots.sum(0)
+        return torch.cat([slots[:, :ns].sum(0), slots[:, ns:].amax(0)])
+
     def _reduce_globals(self):
         with trace.span("globals"):
-            g = self.comm.allreduce_globals(self.globals_t, self.model.n_sum_globals)
+            g = self.comm.allreduce_globals(self.globals_vector(), self.model.n_sum_globals)
         vals = g.detach().cpu().numpy()
         for i, gl in enumerate(self.model.globals_):
             self.globals[gl.name] = float(vals[i])

@@ -17,6 +17,12 @@ from typing import Dict, Optional
 import torch  # noqa: F401  (must be imported before loading HIP libraries)
 
 MIRROR_FIELDS = 128     # core.hpp TCLB_MIRROR_FIELDS
+GSLOTS = 64             # core.hpp TCLB_GSLOTS: globals accumulate in GSLOTS slots ...
+
+
+def gstride(ng: int) -> int:
+    """... of gstride(NG) doubles each (core.hpp gstride)"""
+    return (ng + 15) // 16 * 16
 
 
 class Launch(ctypes.Structure):
