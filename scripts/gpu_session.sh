@@ -54,6 +54,16 @@ refcases)
 annular)
   step "annular Taylor bubble 3000 its, output as written" 600 $O/annular_output.jsonl python tools/run_examples.py --device cuda --iters 3000 --out /tmp/tclb_ex $R/_refcases/d3q27_pf_velocity/annularTaylorBubble_DasC.xml
   step "annular Taylor bubble 3000 its, no output" 600 $O/annular_nooutput.jsonl python tools/run_examples.py --device cuda --iters 3000 --no-output --out /tmp/tclb_ex2 $R/_refcases/d3q27_pf_velocity/annularTaylorBubble_DasC.xml ;;
+globab)
+  step "bench fp64" 300 $O/bench_fp64.json python bench.py --steps 50
+  step "bench fp64 globals every step" 300 $O/bench_fp64_globevery.json python bench.py --steps 50 --glob-every-step
+  step "bench mixed-shift" 300 $O/bench_ms.json python bench.py --steps 50 --precision mixed-shift
+  step "bench mixed-shift globals every step" 300 $O/bench_ms_globevery.json python bench.py --steps 50 --precision mixed-shift --glob-every-step
+  step "rocprof globals every step" 400 $O/prof_globevery.log rocprofv3 --kernel-trace --stats -d $O/prof_globevery -o run --output-format csv -- python3 $R/bench.py --steps 10 --warmup 2 --glob-every-step ;;
+heavy)
+  step "perf heavy models 256^3 fp64" 600 $O/perf_heavy.log python tools/perf_models.py --models d3q27_tePSM_per_NEBB,d3q27q27_cm_cht,d3q27_pf_velocity_thermo,d3q27_pf_velocity_OutFlow,d3q27_pf_velocity --n3 256 --steps 10
+  step "counters heavy models" 600 $O/counters_heavy.log python tools/counters.py --tag r03_heavy_256 --nodes 16777216 --outdir $O/counters -- python3 $R/tools/perf_models.py --models d3q27_tePSM_per_NEBB,d3q27q27_cm_cht,d3q27_pf_velocity_thermo --n3 256 --steps 3
+  step "counters cavity 256" 400 $O/counters_cavity.log python tools/counters.py --tag r03_cavity_256 --nodes 16777216 --outdir $O/counters -- python3 $R/tools/bench_configs.py --configs cavity --steps 5 --warmup 1 ;;
 smoke) step "smoke" 300 $O/smoke.log python -c "import __graft_entry__ as g; g.smoke()" ;;
 bench1) step "bench fp64" 300 $O/bench_fp64.json python bench.py ;;
 esac; done
