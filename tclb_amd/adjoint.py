@@ -34,7 +34,7 @@ class AdjointError(RuntimeError):
 
 
 class Adjoint:
-    def __init__(self, lat, settings: Sequence[str] = (), zonal: Sequence[str] = ()):
+    def __init__(self, lat, settings: Sequence[str] = (), zonal: Sequence[str] = (), reverse: bool = True):
         if lat.sdtype != torch.float64:
             raise AdjointError("adjoint needs double precision storage")
         self.lat = lat
@@ -52,6 +52,10 @@ class Adjoint:
         # the GPU executor reads its context from device memory
         self._ad_cover = {}   # stage -> largest input count of a node (GPU pass sizing)
         self._ctx_dev = torch.zeros(ctypes.sizeof(abi.AdCtx), dtype=torch.uint8, device=dev) if lat.is_gpu else None
+        # reverse sweeps of the model (Model.set_reverse) are used when no setting is seeded;
+        # reverse=False forces the dual-number passes everywhere (tests, A/B)
+        self.reverse = bool(lat.model.reverse) and reverse
+        self._seeded = bool(list(settings) or list(zonal))
 
     # ------------------------------------------------------------------ one action
     def _ad_stage(self, si: int, inp: torch.Tensor, aout: torch.Tensor, obj_weight: float) -> torch.Tensor:
@@ -84,6 +88,9 @@ class Adjoint:
         # earlier call (0 = all TCLB_AD_K); the device reports the count in AdCtx.reserved
         cover = self._ad_cover.get(si, 0) if self._ctx_dev is not None else 0
         L.reserved0 = cover
+        # hand-written reverse sweeps (Model.set_reverse) on the nodes they cover, unless a
+        # setting gradient is asked for (the sweeps push state adjoints only)
+        L.next[5] = 1 if (self.reverse and not self._seeded) else 0
         L.stream = lat._stream()
         if self._ctx_dev is not None:
             self._ctx_dev.copy_(torch.frombuffer(bytearray(bytes(c)), dtype=torch.uint8))
@@ -101,14 +108,15 @@ class Adjoint:
         if self._ctx_dev is not None:
             c = abi.AdCtx.from_buffer_copy(bytes(self._ctx_dev.cpu().numpy()))
             w = self.lib.window
-            covered = -(-cover // w) * w if cover else self.lib.tangents
+            covered = -(-cover // w) * w if cover > 0 else (w if cover < 0 else self.lib.tangents)
             if c.reserved > covered:
                 # a node read more inputs than the windows covered: the windows partition the
                 # Jacobian columns, so the missing ones are added by the remaining windows
                 L.reserved2, L.reserved0 = covered, 0
                 self.lib.run(L)
                 c = abi.AdCtx.from_buffer_copy(bytes(self._ctx_dev.cpu().numpy()))
-            self._ad_cover[si] = max(cover, c.reserved)
+            # -1: no node of this stage needed the dual passes (every node swept in reverse)
+            self._ad_cover[si] = max(cover, c.reserved) if (c.reserved or not L.next[5]) else -1
         if c.overflow:
             raise AdjointError(f"model {lat.model.name}: a node needed more than {self.lib.tangents} AD tangents")
         lat.reverse_halo(ain)

@@ -118,6 +118,23 @@ struct AdCtx {
   int reserved;
 };
 
+// Adjoint push of a hand-written reverse sweep (Model.set_reverse): a += v at an input's
+// load site (device fp64 atomic / OpenMP atomic).
+TCLB_FN void ad_push(double* p, double v) {
+  if (v == 0.0) return;
+#if TCLB_GPU && defined(__HIP_DEVICE_COMPILE__)
+  unsafeAtomicAdd(p, v);
+#else
+#pragma omp atomic
+  *p += v;
+#endif
+}
+// a node type with a reverse sweep (the emitter defines HAS_REV for models that have one)
+template <class N, class = void>
+struct has_rev { static constexpr bool value = false; };
+template <class N>
+struct has_rev<N, decltype((void)N::HAS_REV)> { static constexpr bool value = N::HAS_REV; };
+
 // Recorder of seeded inputs; no-op for plain real types.
 template <class R>
 struct AdRec {

@@ -24,6 +24,19 @@ inline void ad_stage(const Launch& L) {
     for (int z = L.zlo; z < L.zhi; z++)
       for (int y = L.ylo; y < L.yhi; y++)
         for (int x = L.xlo; x < L.xhi; x++) {
+          if constexpr (has_rev<typename Model::template NodeT<double, double, true>>::value) {
+            // a node with a hand-written reverse sweep (Model.set_reverse; Launch.next[5] = 1
+            // when no setting is seeded): one reverse pass instead of the dual numbers
+            if (L.next[5] == 1) {
+              double gd[NG];
+              for (int i = 0; i < NG; i++) gd[i] = 0.0;
+              typename Model::template NodeT<double, double, true> nr(L, x, y, z, gd);
+              if (nr.template rev_ok<STG>()) {
+                nr.template rev_stage<STG>(*ctx);
+                continue;
+              }
+            }
+          }
           D g[NG];
           for (int i = 0; i < NG; i++) g[i] = i < NSUM ? D(0.0) : D(-1e30);
           typename Model::template NodeT<D, double, true> n(L, x, y, z, g);

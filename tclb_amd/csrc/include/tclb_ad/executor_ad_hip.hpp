@@ -129,7 +129,20 @@ __global__ void __launch_bounds__(AD_BLOCK) k_ad(const Launch L) {
   const int z = L.zlo + (int)blockIdx.z;
   AdCtx* ctx = (AdCtx*)L.ext[5];
   int n = 0;
-  if (x < L.xhi) {
+  bool rev = false;
+  if constexpr (has_rev<typename Model::template NodeT<double, double, true>>::value) {
+    // nodes with a hand-written reverse sweep (Model.set_reverse; Launch.next[5] = 1 when
+    // no setting is seeded) run it once, in the first window launch, and skip the dual
+    // passes of every window
+    if (x < L.xhi && L.next[5] == 1) {
+      double gd[NG > 0 ? NG : 1];
+      for (int i = 0; i < NG; i++) gd[i] = 0.0;
+      typename Model::template NodeT<double, double, true> nr(L, x, y, z, gd);
+      rev = nr.template rev_ok<STG>();
+      if (rev && L.reserved2 == 0) nr.template rev_stage<STG>(*ctx);
+    }
+  }
+  if (x < L.xhi && !rev) {
     D g[NG];
     for (int i = 0; i < NG; i++) g[i] = i < NSUM ? D(0.0) : D(-1e30);
     typename Model::template NodeT<D, double, true> nd(L, x, y, z, g);
@@ -153,7 +166,8 @@ inline int ad_hip_impl(const Launch& L, std::integer_sequence<int, I...>) {
   const dim3 grid((w + AD_BLOCK - 1) / AD_BLOCK, h, d), block(AD_BLOCK, 1, 1);
   hipStream_t s = (hipStream_t)L.stream;
   // windows [L.reserved2, L.reserved0) of the input list (reserved0 = 0: all TCLB_AD_K)
-  const int end = (L.reserved0 > 0 && L.reserved0 < TCLB_AD_K) ? L.reserved0 : TCLB_AD_K;
+  // (reserved0 < 0: every node of the stage runs its reverse sweep: one launch)
+  const int end = L.reserved0 < 0 ? 1 : ((L.reserved0 > 0 && L.reserved0 < TCLB_AD_K) ? L.reserved0 : TCLB_AD_K);
   for (int base = L.reserved2; base < end; base += TCLB_AD_WINDOW) {
     Launch Lb = L;
     Lb.reserved2 = base;

@@ -143,6 +143,9 @@ class Model:
         self.options: Dict[str, bool] = {}
         self.dynamics: Optional[str] = None          # include path (relative to csrc/models)
         self.codegen_blocks: List[Callable[["Model"], str]] = []
+        # hand-written reverse-mode node adjoints: stage main -> (predicate, function)
+        # member names in the dynamics (see set_reverse)
+        self.reverse: Dict[str, tuple] = {}
         self.lattices: Dict[str, str] = {}           # group -> lattice name (weights table)
         self.defines: Dict[str, str] = {}
         self.objectives: Dict[str, str] = {}        # AddObjective: name -> expression of globals
@@ -287,6 +290,14 @@ class Model:
 
     def set_dynamics(self, include: str):
         self.dynamics = include
+
+    def set_reverse(self, stage_main: str, predicate: str, function: str):
+        """reverse-mode adjoint of the stages running ``stage_main``: on nodes where the
+        dynamics' ``predicate()`` holds, the AD executors call ``function(const AdCtx&)``
+        (one reverse sweep of the node: transposed Jacobian-vector product pushed to the
+        load sites) instead of the forward-mode dual-number passes; the reference gets
+        its reverse sweep from Tapenade (tools/makeAD)"""
+        self.reverse[stage_main] = (predicate, function)
 
     def add_codegen(self, fn: Callable[["Model"], str]):
         self.codegen_blocks.append(fn)

@@ -6,6 +6,15 @@ Reference: models/optimization/d3q19_adj/{Dynamics.R, Dynamics.c.Rt} (ADJOINT=1)
 from ..dsl import Model
 from ...emit.symbolic import d3q19_mrt
 from ..flow.d3q19 import mrt19_block
+from ...emit.blocks import dense_transform
+
+
+def mrt19_transposes(_m):
+    """transposes of the moment maps for the reverse sweep (rev_run): a_f = M^T a_m and
+    a_m = (M^-1)^T a_f"""
+    M = d3q19_mrt().MAT
+    return "\n".join([dense_transform("mrt_moments_T", M.T, 19, 19, "a_f = a_m . MRTMAT^T"),
+                      dense_transform("mrt_inverse_T", M.inv().T, 19, 19, "a_m = a_f . (MRTMAT^-1)^T")])
 
 
 def build() -> Model:
@@ -37,5 +46,7 @@ def build() -> Model:
     m.add_node_type("MRT", "COLLISION")
     m.add_node_type("DesignSpace", "DESIGNSPACE")
     m.add_codegen(mrt19_block)
+    m.add_codegen(mrt19_transposes)
     m.set_dynamics("optimization/d3q19_adj.inc")
+    m.set_reverse("Run", "rev_ok_run", "rev_run")
     return m
