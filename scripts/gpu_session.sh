@@ -64,6 +64,16 @@ heavy)
   step "perf heavy models 256^3 fp64" 600 $O/perf_heavy.log python tools/perf_models.py --models d3q27_tePSM_per_NEBB,d3q27q27_cm_cht,d3q27_pf_velocity_thermo,d3q27_pf_velocity_OutFlow,d3q27_pf_velocity --n3 256 --steps 10
   step "counters heavy models" 600 $O/counters_heavy.log python tools/counters.py --tag r03_heavy_256 --nodes 16777216 --outdir $O/counters -- python3 $R/tools/perf_models.py --models d3q27_tePSM_per_NEBB,d3q27q27_cm_cht,d3q27_pf_velocity_thermo --n3 256 --steps 3
   step "counters cavity 256" 400 $O/counters_cavity.log python tools/counters.py --tag r03_cavity_256 --nodes 16777216 --outdir $O/counters -- python3 $R/tools/bench_configs.py --configs cavity --steps 5 --warmup 1 ;;
+r03m)
+  step "configs fp64 (cavity, pf384, part256)" 600 $O/configs_fp64.log python tools/bench_configs.py
+  step "configs mixed-shift pf384" 400 $O/configs_pf384_ms.log python tools/bench_configs.py --configs pf384 --precision mixed-shift
+  step "YZ grid loopback 512x256x128" 300 $O/yz_loop.json env TCLB_GRID=1,1 python bench.py --shape 512,256,128 --steps 50 --warmup 5 --loopback-dist
+  step "plain 512x256x128" 300 $O/yz_plain.json python bench.py --shape 512,256,128 --steps 50 --warmup 5
+  step "rocprof YZ grid loopback" 400 $O/prof_yz.log env TCLB_GRID=1,1 rocprofv3 --kernel-trace --stats -d $O/prof_yz -o run --output-format csv -- python3 $R/bench.py --shape 512,256,128 --steps 10 --warmup 2 --loopback-dist ;;
+adjrev)
+  step "gpu adjoint tests" 600 $O/pytest_gpu_adjoint.log python -u -m pytest tests/test_gpu_adjoint.py tests/test_adjoint_reverse.py tests/test_adjoint_dist.py -v -m gpu --timeout 300 --timeout-method thread
+  step "adjoint bench 128" 400 $O/bench_adjoint_128.json python tools/bench_adjoint.py --size 128 --steps 80
+  step "rocprof adjoint 128" 400 $O/prof_adjoint.log rocprofv3 --kernel-trace --stats -d $O/prof_adjoint -o run --output-format csv -- python3 $R/tools/bench_adjoint.py --size 128 --steps 20 ;;
 smoke) step "smoke" 300 $O/smoke.log python -c "import __graft_entry__ as g; g.smoke()" ;;
 bench1) step "bench fp64" 300 $O/bench_fp64.json python bench.py ;;
 esac; done

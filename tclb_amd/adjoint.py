@@ -56,11 +56,26 @@ class Adjoint:
         # reverse=False forces the dual-number passes everywhere (tests, A/B)
         self.reverse = bool(lat.model.reverse) and reverse
         self._seeded = bool(list(settings) or list(zonal))
+        self._abuf = None             # persistent (aout, ain) buffers of _ad_stage
+        self._ctx_bytes = b""
+        self._ovf = torch.zeros(1, dtype=torch.int32, device=dev) if lat.is_gpu else None
 
     # ------------------------------------------------------------------ one action
     def _ad_stage(self, si: int, inp: torch.Tensor, aout: torch.Tensor, obj_weight: float) -> torch.Tensor:
+        """adjoint of one stage launch: returns a new tensor dJ/d(stage inputs).
+
+        The adjoint buffers the executor reads and writes are persistent (their addresses
+        sit in the AdCtx, which is uploaded only when it changes) and the AdCtx is read
+        back only on the first call of a stage (to size the tangent windows): the later
+        calls of an adjoint sweep run without a host synchronisation; window overflow is
+        accumulated on the device and checked once per sweep (check_overflow)."""
         lat = self.lat
-        ain = torch.zeros_like(aout)
+        if self._abuf is None:
+            self._abuf = (torch.zeros_like(aout), torch.zeros_like(aout))
+        aout_b, ain = self._abuf
+        if aout is not aout_b:
+            aout_b.copy_(aout)
+        ain.zero_()
         L = lat._base_launch()
         lat._sync_settings()
         L.settings = lat.settings_t.data_ptr()
@@ -74,7 +89,7 @@ class Adjoint:
         L.iter = lat.iter
         L.globals_ = lat.globals_t.data_ptr()
         c = self.ctx
-        c.aout = aout.data_ptr()
+        c.aout = aout_b.data_ptr()
         c.ain = ain.data_ptr()
         c.gset = self.gset.data_ptr()
         c.gzon = self.gzon.data_ptr()
@@ -92,8 +107,12 @@ class Adjoint:
         # setting gradient is asked for (the sweeps push state adjoints only)
         L.next[5] = 1 if (self.reverse and not self._seeded) else 0
         L.stream = lat._stream()
+        first = si not in self._ad_cover
         if self._ctx_dev is not None:
-            self._ctx_dev.copy_(torch.frombuffer(bytearray(bytes(c)), dtype=torch.uint8))
+            raw = bytes(c)
+            if first or raw != self._ctx_bytes:
+                self._ctx_dev.copy_(torch.frombuffer(bytearray(raw), dtype=torch.uint8))
+                self._ctx_bytes = raw
             L.ext[5] = self._ctx_dev.data_ptr()
         else:
             L.ext[5] = ctypes.cast(ctypes.pointer(c), ctypes.c_void_p)
@@ -106,21 +125,46 @@ class Adjoint:
             L.next[1] = lat.cuts.numel()
         self.lib.run(L)
         if self._ctx_dev is not None:
-            c = abi.AdCtx.from_buffer_copy(bytes(self._ctx_dev.cpu().numpy()))
-            w = self.lib.window
-            covered = -(-cover // w) * w if cover > 0 else (w if cover < 0 else self.lib.tangents)
-            if c.reserved > covered:
-                # a node read more inputs than the windows covered: the windows partition the
-                # Jacobian columns, so the missing ones are added by the remaining windows
-                L.reserved2, L.reserved0 = covered, 0
-                self.lib.run(L)
+            if first:
                 c = abi.AdCtx.from_buffer_copy(bytes(self._ctx_dev.cpu().numpy()))
-            # -1: no node of this stage needed the dual passes (every node swept in reverse)
-            self._ad_cover[si] = max(cover, c.reserved) if (c.reserved or not L.next[5]) else -1
-        if c.overflow:
+                w = self.lib.window
+                covered = -(-cover // w) * w if cover > 0 else (w if cover < 0 else self.lib.tangents)
+                if c.reserved > covered:
+                    # a node read more inputs than the windows covered: the windows partition
+                    # the Jacobian columns, so the missing ones are added by the remaining windows
+                    L.reserved2, L.reserved0 = covered, 0
+                    self.lib.run(L)
+                    c = abi.AdCtx.from_buffer_copy(bytes(self._ctx_dev.cpu().numpy()))
+                # -1: no node of this stage needed the dual passes (every node swept in reverse)
+                self._ad_cover[si] = max(cover, c.reserved) if (c.reserved or not L.next[5]) else -1
+                if c.overflow:
+                    raise AdjointError(f"model {lat.model.name}: a node needed more than "
+                                       f"{self.lib.tangents} AD tangents")
+            else:
+                # the device sets AdCtx.overflow; keep it (the next upload resets it)
+                o = abi.ADCTX_OVERFLOW_OFFSET
+                flag = self._ctx_dev[o:o + 4].view(torch.int32)
+                torch.maximum(self._ovf, flag, out=self._ovf)
+        elif c.overflow:
             raise AdjointError(f"model {lat.model.name}: a node needed more than {self.lib.tangents} AD tangents")
         lat.reverse_halo(ain)
-        return ain
+        return ain.clone()
+
+    def _free_bytes(self) -> float:
+        if self.lat.is_gpu:
+            return float(torch.cuda.mem_get_info(self.lat.device)[0])
+        try:
+            import psutil
+            return float(psutil.virtual_memory().available)
+        except ImportError:      # pragma: no cover
+            return 8e9
+
+    def check_overflow(self):
+        """raise if any dual-number node of the sweeps since the last check needed more
+        tangents than the executor has (one host synchronisation)"""
+        if self._ovf is not None and int(self._ovf.item()):
+            self._ovf.zero_()
+            raise AdjointError(f"model {self.lat.model.name}: a node needed more than {self.lib.tangents} AD tangents")
 
     def step_back(self, a_next: torch.Tensor, action: str = "Iteration", obj_weight: float = 1.0,
                   state: Optional[torch.Tensor] = None) -> torch.Tensor:
@@ -167,33 +211,62 @@ class Adjoint:
                  a_final: Optional[torch.Tensor] = None) -> torch.Tensor:
         """run `steps` primal iterations from the current state recording checkpoints,
         then sweep backwards; returns dJ/d(initial state).  The primal ends at its final
-        state (as the reference's record/rewind leaves it)."""
+        state (as the reference's record/rewind leaves it).
+
+        Two-level checkpointing: a snapshot every `checkpoint` (default sqrt(steps))
+        iterations; the reverse sweep re-runs each segment once, keeping its states (the
+        288 GB of HBM hold sqrt(steps) snapshots easily), so every primal step is
+        recomputed once instead of once per later step of its segment.  The Objective is
+        summed on the device (no host round trip per recorded step)."""
         lat = self.lat
         checkpoint = checkpoint or max(1, int(math.sqrt(steps)))
+        # memory: (steps / checkpoint) checkpoints + one segment of states; when that does
+        # not fit in half the free memory, keep only checkpoints and re-run each reverse
+        # step from its checkpoint instead (no segment states)
+        snap_bytes = lat.snaps[0].numel() * lat.snaps[0].element_size()
+        keep_segment = (steps // checkpoint + checkpoint + 2) * snap_bytes <= 0.5 * self._free_bytes()
         it0 = lat.iter
         snaps: Dict[int, torch.Tensor] = {0: lat.snaps[lat.cur].clone()}
-        self.J = 0.0
+        obj = next((i for i, g in enumerate(lat.model.globals_) if g.name == "Objective"), None)
+        J = torch.zeros((), dtype=torch.float64, device=lat.device)
         for t in range(steps):
-            lat.iterate(1, glob_last=True, action=action)
-            self.J += lat.globals.get("Objective", 0.0)
+            lat.iterate(1, glob_last=True, action=action, reduce=False)
+            if obj is not None:
+                J += lat.globals_vector()[obj]
             if (t + 1) % checkpoint == 0 and t + 1 < steps:
                 snaps[t + 1] = lat.snaps[lat.cur].clone()
+        lat._reduce_globals()
+        self.J = lat.comm.allreduce_scalar(float(J.item()), "sum") if obj is not None else 0.0
         final = lat.snaps[lat.cur].clone()
         cur_final = lat.cur
         a = torch.zeros_like(final) if a_final is None else a_final
-        for t in range(steps - 1, -1, -1):
-            base = max(k for k in snaps if k <= t)
+        bases = sorted(snaps)
+        for si, base in reversed(list(enumerate(bases))):
+            end = bases[si + 1] if si + 1 < len(bases) else steps
+            # re-run the segment once, keeping the state before every step
             lat.snaps[lat.cur].copy_(snaps[base])
             lat.iter = it0 + base
-            for _ in range(t - base):
+            states = [snaps[base]]
+            for t in range(base + 1, end if keep_segment else base + 1):
                 lat.iterate(1, glob_last=False, action=action)
-            lat.iter = it0 + t
-            if lat.zseries:
-                lat.apply_series()
-                before = self.gzon.cpu().numpy().copy()
-            a = self.step_back(a, action)
-            if lat.zseries:
-                self._series_grad(before, lat)
+                states.append(lat.snaps[lat.cur].clone())
+            for t in range(end - 1, base - 1, -1):
+                if keep_segment:
+                    lat.snaps[lat.cur].copy_(states[t - base])
+                else:
+                    lat.snaps[lat.cur].copy_(snaps[base])
+                    lat.iter = it0 + base
+                    for _ in range(t - base):
+                        lat.iterate(1, glob_last=False, action=action)
+                lat.iter = it0 + t
+                if lat.zseries:
+                    lat.apply_series()
+                    before = self.gzon.cpu().numpy().copy()
+                a = self.step_back(a, action)
+                if lat.zseries:
+                    self._series_grad(before, lat)
+            del states
+        self.check_overflow()
         lat.snaps[cur_final].copy_(final)
         lat.cur = cur_final
         lat.iter = it0 + steps
@@ -244,6 +317,7 @@ class Adjoint:
             a = b
             if tol and d < tol:
                 break
+        self.check_overflow()
         self.a0 = a
         self.lat.adjoint_state = a
         return a

@@ -467,7 +467,9 @@ class Lattice:
     def _saved_fields(self, stage) -> List[int]:
         return [i for i, f in enumerate(self.model.fields) if self.model.matches(f, stage.save_fields)]
 
-    def run_action(self, name: str, glob: bool = False):
+    def run_action(self, name: str, glob: bool = False, reduce: bool = True):
+        """one action; with glob the globals are integrated and (reduce) all-reduced and
+        copied to the host (reduce=False leaves them on the device: globals_vector())"""
         m = self.model
         act = m.action(name)
         if act is None:
@@ -536,7 +538,7 @@ class Lattice:
             if trace.ENABLED:
                 trace.pop()
         self.cur = 1 - self.cur
-        if glob:
+        if glob and reduce:
             self._reduce_globals()
         if trace.ENABLED:
             trace.pop()
@@ -577,7 +579,7 @@ class Lattice:
         return act is not None and not any(self.model.stage(s).fixed_point or self.model.stage(s).particle or
                                            self.model.stage(s).snapshot_reads for s in act.stages)
 
-    def iterate(self, n: int, glob_last: bool = True, action: str = "Iteration"):
+    def iterate(self, n: int, glob_last: bool = True, action: str = "Iteration", reduce: bool = True):
         """Reference Lattice::Iterate (src/Lattice.cu.Rt:900-989): globals on the last step.
 
         Without halos, time series, callbacks or particles the n steps run in one native
@@ -608,14 +610,14 @@ class Lattice:
             self.iter += n
             if n % 2 == 1:
                 self.cur = 1 - self.cur
-            if glob_last:
+            if glob_last and reduce:
                 self._reduce_globals()
             return
         for i in range(n):
             glob = glob_last and i == n - 1
             if self.zseries:
                 self.apply_series()
-            self.run_action(action, glob=glob)
+            self.run_action(action, glob=glob, reduce=reduce)
             self.iter += 1
             for smp in self.samplers:
                 smp.sample_now()

@@ -118,6 +118,9 @@ class AdCtx(ctypes.Structure):
     ]
 
 
+ADCTX_OVERFLOW_OFFSET = AdCtx.overflow.offset
+
+
 class AdLib:
     """the adjoint (AD) executor library of one model: libtclb_<model>_ad.so (CPU) or
     libtclb_<model>_adhip.so (GPU, tclb_ad/executor_ad_hip.hpp)"""
