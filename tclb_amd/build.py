@@ -309,12 +309,14 @@ def _write_src_stamp(name: str, kind: str, variant: str, s: Optional[str] = None
 
 
 def build_host(force: bool = False, verbose: bool = False) -> str:
-    """native host runtime library (geometry voxeliser, scans): libtclb_host.so"""
-    src = os.path.join(CSRC, "runtime", "host.cpp")
+    """native host runtime library (geometry voxeliser, scans, HDF5 writer): libtclb_host.so
+    from every csrc/runtime/*.cpp"""
+    rdir = os.path.join(CSRC, "runtime")
+    srcs = sorted(os.path.join(rdir, f) for f in os.listdir(rdir) if f.endswith(".cpp"))
     target = os.path.join(LIB, "libtclb_host.so")
     os.makedirs(LIB, exist_ok=True)
-    cmd = [CXX, "-O3", "-std=c++17", "-fPIC", "-shared", "-fopenmp", src, "-o", target + ".tmp"]
-    h = _hash_inputs([src], " ".join(cmd))
+    cmd = [CXX, "-O3", "-std=c++17", "-fPIC", "-shared", "-fopenmp", *srcs, "-o", target + ".tmp"]
+    h = _hash_inputs(srcs, " ".join(cmd))
     stamp = target + ".hash"
     if not force and os.path.exists(target) and os.path.exists(stamp) and open(stamp).read() == h:
         return target

@@ -247,10 +247,11 @@ class VTK(Callback):
 
 @register("HDF5")
 class HDF5(Callback):
-    """reference cbHDF5 (src/Handlers/cbHDF5.cpp): region-cropped field output with an
-    XDMF sidecar.  libhdf5/h5py are not part of this image, so the data go to one raw
-    binary file per step that the .xmf describes (readable by ParaView/VisIt);
-    ``compress`` / ``chunk`` / ``point_data`` are accepted and ignored with a notice."""
+    """reference cbHDF5 (src/Handlers/cbHDF5.cpp): region-cropped field output, one HDF5
+    file per step (written by the native writer csrc/runtime/h5.cpp, no libhdf5) with an
+    XDMF sidecar (``write_xdmf``).  Datasets are stored contiguous: ``compress`` (deflate)
+    and ``chunk`` are accepted and ignored with a notice, as is ``point_data``;
+    ``format="binary"`` writes a raw binary file plus .xmf instead."""
 
     def init(self):
         super().init()
@@ -266,11 +267,14 @@ class HDF5(Callback):
             raise HandlerError("HDF5 precision should be double or float")
         for a in ("compress", "chunk", "point_data"):
             if self.node.get(a) is not None:
-                log.notice(f"HDF5: attribute {a} has no effect with the XDMF+binary container")
+                log.notice(f"HDF5: attribute {a} has no effect (contiguous datasets)")
+        self.hdf5 = self.node.get("format", "hdf5").lower() != "binary"
+        self.xdmf = self.node.get("write_xdmf", "true").lower() in ("true", "1", "yes")
         return 0
 
     def do_it(self):
-        return self.solver.write_xdmf(self.name, self.what, self.reg, double=self.double)
+        return self.solver.write_xdmf(self.name, self.what, self.reg, double=self.double, hdf5=self.hdf5,
+                                      write_xdmf=self.xdmf)
 
 
 @register("Catalyst")

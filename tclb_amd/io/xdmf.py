@@ -54,7 +54,9 @@ def write_piece(path: str, region, lreg, fields, lay):
         os.close(fd)
 
 
-def write_xmf(path: str, binname: str, region, lay, spacing: float = 1.0, time: float = 0.0):
+def write_xmf(path: str, binname: str, region, lay, spacing: float = 1.0, time: float = 0.0, hdf5: bool = False):
+    """XDMF sidecar; hdf5=True: the DataItems point into an HDF5 file ("file.h5:/Name", as
+    the reference's hdf5WriteLattice), else into the raw binary file at byte offsets"""
     X0, Y0, Z0, nx, ny, nz = region
     lines = ['<?xml version="1.0" ?>', '<!DOCTYPE Xdmf SYSTEM "Xdmf.dtd" []>', '<Xdmf Version="2.0">', '<Domain>',
              '<Grid Name="lattice" GridType="Uniform">', f'<Time Value="{time:g}"/>',
@@ -66,9 +68,13 @@ def write_xmf(path: str, binname: str, region, lay, spacing: float = 1.0, time: 
     for name, dt, nc, off in lay:
         at = "Vector" if nc == 3 else "Scalar"
         dims = f"{nz} {ny} {nx}" + (f" {nc}" if nc > 1 else "")
-        lines += [f'<Attribute Name="{name}" AttributeType="{at}" Center="Cell">',
-                  f'<DataItem Dimensions="{dims}" NumberType="{_XT[dt.kind]}" Precision="{dt.itemsize}" '
-                  f'Endian="Little" Format="Binary" Seek="{off}">{binname}</DataItem>', '</Attribute>']
+        if hdf5:
+            item = (f'<DataItem Dimensions="{dims}" NumberType="{_XT[dt.kind]}" Precision="{dt.itemsize}" '
+                    f'Format="HDF">{binname}:/{name}</DataItem>')
+        else:
+            item = (f'<DataItem Dimensions="{dims}" NumberType="{_XT[dt.kind]}" Precision="{dt.itemsize}" '
+                    f'Endian="Little" Format="Binary" Seek="{off}">{binname}</DataItem>')
+        lines += [f'<Attribute Name="{name}" AttributeType="{at}" Center="Cell">', item, '</Attribute>']
     lines += ['</Grid>', '</Domain>', '</Xdmf>']
     with open(path, "w") as f:
         f.write("\n".join(lines) + "\n")
@@ -82,6 +88,10 @@ def read_field(xmf_path: str, name: str) -> np.ndarray:
         if at.get("Name") == name:
             di = at.find("DataItem")
             dims = [int(v) for v in di.get("Dimensions").split()]
+            if di.get("Format") == "HDF":
+                from .h5read import read_h5
+                fn, _, ds = di.text.strip().partition(":/")
+                return read_h5(os.path.join(os.path.dirname(xmf_path), fn))[ds].reshape(dims)
             kind = {"Float": "f", "UInt": "u", "Int": "i"}[di.get("NumberType")]
             dt = np.dtype(f"<{kind}{di.get('Precision')}")
             with open(os.path.join(os.path.dirname(xmf_path), di.text.strip()), "rb") as f:

@@ -26,6 +26,8 @@ def lib():
             L.tclb_stl_fill.restype = ctypes.c_longlong
             L.tclb_stl_cuts.argtypes = [P, i, i, i, i, i, i, i, P, P, P]
             L.tclb_stl_cuts.restype = ctypes.c_longlong
+            L.tclb_h5_create.argtypes = [ctypes.c_char_p, i, ctypes.c_char_p, P, P, P, P]
+            L.tclb_h5_create.restype = ctypes.c_longlong
             L.tclb_solid_grid.argtypes = [P, i, i, i, i, i, i, P, ctypes.c_longlong]
             L.tclb_solid_grid.restype = ctypes.c_longlong
             L.tclb_nan_scan_f64.argtypes = [P, ctypes.c_longlong]
@@ -77,3 +79,23 @@ def solid_grid(rec: np.ndarray, shape, cell: int) -> np.ndarray:
     if r < 0:
         raise RuntimeError("solid grid buffer too small")
     return out[:r]
+
+
+def h5_create(path: str, datasets) -> list:
+    """write the metadata of an HDF5 file (csrc/runtime/h5.cpp) holding contiguous
+    datasets [(name, numpy dtype, shape)], sized for their data; returns the file offset of
+    each dataset's data block"""
+    n = len(datasets)
+    codes = {np.dtype(np.uint8): 0, np.dtype(np.float32): 1, np.dtype(np.float64): 2}
+    names = b"".join(nm.encode() + b"\0" for nm, _, _ in datasets)
+    dt = np.array([codes[np.dtype(t)] for _, t, _ in datasets], dtype=np.int32)
+    rk = np.array([len(s) for _, _, s in datasets], dtype=np.int32)
+    dims = np.zeros((max(1, n), 4), dtype=np.int64)
+    for k, (_, _, s) in enumerate(datasets):
+        dims[k, :len(s)] = s
+    off = np.zeros(max(1, n), dtype=np.int64)
+    r = lib().tclb_h5_create(path.encode(), n, names, dt.ctypes.data, rk.ctypes.data, dims.ctypes.data,
+                              off.ctypes.data)
+    if r < 0:
+        raise OSError(f"cannot write {path}")
+    return [int(v) for v in off[:n]]

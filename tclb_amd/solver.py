@@ -252,11 +252,14 @@ class Solver:
             vtk.write_pvti(fn[:-4] + ".pvti", region, pieces, meta, spacing=spacing)
         return 0
 
-    def write_xdmf(self, name: str, what: Optional[Sequence[str]], region=None, double: bool = True):
-        """HDF5-callback output without libhdf5: one raw little-endian binary file holding
-        every selected field of the region (each rank pwrite()s its own slab rows) and an
-        XDMF sidecar that ParaView/VisIt open directly (reference hdf5WriteLattice + XDMF,
-        src/hdf5Lattice.cpp:26-339)."""
+    def write_xdmf(self, name: str, what: Optional[Sequence[str]], region=None, double: bool = True,
+                   hdf5: bool = True, write_xdmf: bool = True):
+        """HDF5 callback output (reference hdf5WriteLattice + XDMF, src/hdf5Lattice.cpp:26-339):
+        one HDF5 file per step with a contiguous dataset per flag group (uint8) and per
+        selected quantity (vectors (nz, ny, nx, 3)) over the output region, written by the
+        native writer (csrc/runtime/h5.cpp: rank 0 lays out the metadata, every rank
+        pwrite()s its own slab rows into the data blocks), and an XDMF sidecar.  hdf5=False
+        writes the same blocks as one raw binary file instead."""
         from .io import xdmf
         lat = self.lattice
         fields = self.output_fields(what)
@@ -264,24 +267,38 @@ class Solver:
         sx, sy, sz = lat.slab.offset
         nx, ny, nz = lat.shape
         sub = _crop(fields, (sx, sy, sz, nx, ny, nz), region)
-        base = self.out_iter_file(name, "")
+        # one collective file per step, as the reference's outIterCollectiveFile(nm, ".h5")
+        base = self.out_iter_collective_file(name, "")
         spacing = 1.0 / self.units.alt("1m") if self.units.alt("1m") != 0 else 1.0
         dt = np.float64 if double else np.float32
         meta = [(n, (np.dtype(dt) if np.asarray(a).dtype.kind == "f" else np.asarray(a).dtype), nc)
                 for n, a, nc in fields]
         layout = xdmf.layout(region, meta)
-        if self.rank == 0:
+        data = base + (".h5" if hdf5 else ".bin")
+        if hdf5:
+            # dataset data blocks at the offsets the native writer chose (rank 0)
+            from .ops.host import h5_create
+            _, _, _, rnx, rny, rnz = region
+            shapes = [(n, dt, (rnz, rny, rnx) + ((nc,) if nc > 1 else ())) for n, dt, nc, _ in layout]
+            offs = None
+            if self.rank == 0:
+                log.output(f"{self.iter:8d} it writing hdf5 {data}")
+                os.makedirs(os.path.dirname(data) or ".", exist_ok=True)
+                offs = h5_create(data, shapes)
+            offs = self.comm.bcast_object(offs)
+            layout = [(n, dt, nc, o) for (n, dt, nc, _), o in zip(layout, offs)]
+        elif self.rank == 0:
             log.output(f"{self.iter:8d} it writing xdmf {base}.xmf")
-            xdmf.create(base + ".bin", layout)
+            xdmf.create(data, layout)
         self.comm.barrier()
         if sub is not None:
             lreg, lfields = sub
-            xdmf.write_piece(base + ".bin", region, lreg, [(n, np.asarray(a).astype(t, copy=False), nc)
-                                                         for (n, a, nc), (_, t, _) in zip(lfields, meta)], layout)
+            xdmf.write_piece(data, region, lreg, [(n, np.asarray(a).astype(t, copy=False), nc)
+                                                for (n, a, nc), (_, t, _) in zip(lfields, meta)], layout)
         self.comm.barrier()
-        if self.rank == 0:
-            xdmf.write_xmf(base + ".xmf", os.path.basename(base) + ".bin", region, layout, spacing,
-                           time=self.iter * self.units.alt("1s") if self.units.alt("1s") else self.iter)
+        if self.rank == 0 and (write_xdmf or not hdf5):
+            xdmf.write_xmf(base + ".xmf", os.path.basename(data), region, layout, spacing,
+                           time=self.iter * self.units.alt("1s") if self.units.alt("1s") else self.iter, hdf5=hdf5)
         return 0
 
     def write_txt(self, name: str, what: Optional[Sequence[str]], gzip: bool = False):

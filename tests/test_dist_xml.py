@@ -106,6 +106,13 @@ def test_d3q27_xml_vtk_log_sample_checkpoint(tmp_path):
     la, lb = (_csv(d / "output" / "channel3d_Log_P00_00000000.csv") for d in (one, four))
     assert la[0] == lb[0] and len(la) == len(lb) == 4
     np.testing.assert_allclose(np.array(lb[1:], float), np.array(la[1:], float), rtol=1e-10, atol=1e-15)
+    # HDF5 written by 4 ranks into one file (each its own slab rows) equals the 1-rank file
+    from tclb_amd.io.h5read import read_h5
+    h1 = read_h5(str(one / "output" / "channel3d_HDF5_00000030.h5"))
+    h4 = read_h5(str(four / "output" / "channel3d_HDF5_00000030.h5"))
+    assert sorted(h1) == sorted(h4) and "U" in h1
+    for k in h1:
+        assert np.array_equal(h1[k], h4[k]), k
     sa = open(one / "output" / "channel3d_Sampler_P00_00000000.csv").read()
     assert sa == open(four / "output" / "channel3d_Sampler_P00_00000000.csv").read()
     assert len(sa.splitlines()) == 1 + 30 * 3

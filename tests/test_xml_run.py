@@ -116,19 +116,49 @@ def test_deprecated_params_rewrite():
 
 
 def test_hdf5_xdmf_output(tmp_path):
-    """<HDF5> (reference cbHDF5): cropped fields as XDMF + binary; values equal the VTK
-    output of the same step, precision attribute honoured."""
+    """<HDF5> (reference cbHDF5): cropped fields in an HDF5 file with an XDMF sidecar;
+    values equal the VTK output of the same step, precision attribute honoured."""
     from tclb_amd.io.xdmf import read_field
     xml = KARMAN.replace('<Solve Iterations="100"/>',
                          '<HDF5 Iterations="50" dx="10" nx="64" what="U,Rho"/>'
                          '<HDF5 name="F" Iterations="100" precision="float"/><Solve Iterations="100"/>')
     run_case(tmp_path, xml)
     out = tmp_path / "output"
-    x = str(out / "case_HDF5_P00_00000100.xmf")
+    x = str(out / "case_HDF5_00000100.xmf")
     u = read_field(x, "U")
     v = read_vti(str(out / "case_VTK_P00_00000100.vti"))["U"]
     assert u.shape == (1, 32, 64, 3)
     assert np.array_equal(u, v[:, :, 10:74, :])
     assert np.array_equal(read_field(x, "Rho"), read_vti(str(out / "case_VTK_P00_00000100.vti"))["Rho"][:, :, 10:74])
-    f = read_field(str(out / "case_F_P00_00000100.xmf"), "U")
+    f = read_field(str(out / "case_F_00000100.xmf"), "U")
     assert f.dtype == np.float32 and np.allclose(f, v, rtol=1e-6, atol=1e-9)
+    # the container is HDF5 (native writer): every dataset readable by name
+    from tclb_amd.io.h5read import read_h5
+    h = read_h5(str(out / "case_F_00000100.h5"))
+    assert set(h) >= {"U", "Rho", "BOUNDARY", "COLLISION"}
+    assert h["BOUNDARY"].dtype == np.uint8 and h["Rho"].dtype == np.float32
+    assert np.array_equal(h["U"], f)
+
+
+def test_hdf5_writer_many_datasets(tmp_path):
+    """the native HDF5 writer (csrc/runtime/h5.cpp): superblock v0, one symbol-table node
+    for all names (sorted), contiguous blocks of every type; read back by the spec reader"""
+    from tclb_amd.io.h5read import read_h5
+    from tclb_amd.ops.host import h5_create
+    rng = np.random.default_rng(0)
+    arrays = {f"q{k:02d}": rng.normal(size=(3, 4, 5)).astype(np.float64) for k in range(12)}
+    arrays["flags"] = rng.integers(0, 255, size=(3, 4, 5)).astype(np.uint8)
+    arrays["Vec"] = rng.normal(size=(3, 4, 5, 3)).astype(np.float32)
+    names = list(arrays)[::-1]
+    path = str(tmp_path / "t.h5")
+    offs = h5_create(path, [(n, arrays[n].dtype, arrays[n].shape) for n in names])
+    with open(path, "r+b") as fh:
+        for n, o in zip(names, offs):
+            fh.seek(o)
+            fh.write(arrays[n].tobytes())
+    back = read_h5(path)
+    assert sorted(back) == sorted(arrays)
+    for n, a in arrays.items():
+        assert back[n].dtype == a.dtype and np.array_equal(back[n], a), n
+    head = open(path, "rb").read(16)
+    assert head[:8] == b"\x89HDF\r\n\x1a\n" and head[8] == 0
