@@ -69,6 +69,10 @@ r03m)
   step "configs mixed-shift pf384" 400 $O/configs_pf384_ms.log python tools/bench_configs.py --configs pf384 --precision mixed-shift
   step "YZ grid loopback 512x256x128" 300 $O/yz_loop.json env TCLB_GRID=1,1 python bench.py --shape 512,256,128 --steps 50 --warmup 5 --loopback-dist
   step "plain 512x256x128" 300 $O/yz_plain.json python bench.py --shape 512,256,128 --steps 50 --warmup 5
+  step "host overhead: 128^3 plain" 300 $O/ov_plain.json python bench.py --shape 128,128,128 --steps 300 --warmup 20
+  step "host overhead: 128^3 dist path" 300 $O/ov_dist.json python bench.py --shape 128,128,128 --steps 300 --warmup 20 --loopback-dist
+  step "slab 512x512x64 plain" 300 $O/slab_plain.json python bench.py --shape 512,512,64 --steps 200 --warmup 20
+  step "slab 512x512x64 dist path" 300 $O/slab_dist.json python bench.py --shape 512,512,64 --steps 200 --warmup 20 --loopback-dist
   step "rocprof YZ grid loopback" 400 $O/prof_yz.log env TCLB_GRID=1,1 rocprofv3 --kernel-trace --stats -d $O/prof_yz -o run --output-format csv -- python3 $R/bench.py --shape 512,256,128 --steps 10 --warmup 2 --loopback-dist ;;
 adjrev)
   step "gpu adjoint tests" 600 $O/pytest_gpu_adjoint.log python -u -m pytest tests/test_gpu_adjoint.py tests/test_adjoint_reverse.py tests/test_adjoint_dist.py -v -m gpu --timeout 300 --timeout-method thread

@@ -172,6 +172,9 @@ class ParticleSystem:
         acc = self._d["acc"]
         if lat.comm.distributed and lat.comm.size > 1:
             acc.copy_(lat.comm.allreduce_globals(acc.reshape(-1).clone(), acc.numel()).reshape(acc.shape))
+        # a NaN force is dropped (reference Lattice.cu.Rt:420-435 zeroes it with a notice;
+        # the check stays on the device, no host round trip)
+        acc.masked_fill_(torch.isnan(acc), 0.0)
         self._host_stale |= {"force", "torque"}
         self.detach(lat)
 

@@ -53,8 +53,16 @@ class Solver:
         if device is None:
             device = "cuda" if torch.cuda.is_available() else "cpu"
         if device == "cuda":
+            # one GPU per rank of a node (reference main.cpp:318-350): more ranks than GPUs
+            # is refused unless the case sets oversubscribe_gpu="true"
             local = int(os.environ.get("LOCAL_RANK", "0"))
-            self.device = torch.device("cuda", local % max(1, torch.cuda.device_count()))
+            count = max(1, torch.cuda.device_count())
+            if local >= count:
+                if config.get("oversubscribe_gpu", "false").lower() not in ("true", "1", "yes"):
+                    raise SolverError("Oversubscribing GPUs. This is not a good idea, but if you want to do it, "
+                                      'add oversubscribe_gpu="true" to the config file')
+                log.warning("Oversubscribing GPUs.")
+            self.device = torch.device("cuda", local % count)
         else:
             self.device = torch.device(device)
         self.units = UnitEnv()
