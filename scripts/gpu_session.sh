@@ -78,6 +78,9 @@ adjrev)
   step "gpu adjoint tests" 600 $O/pytest_gpu_adjoint.log python -u -m pytest tests/test_gpu_adjoint.py tests/test_adjoint_reverse.py tests/test_adjoint_dist.py -v -m gpu --timeout 300 --timeout-method thread
   step "adjoint bench 128" 400 $O/bench_adjoint_128.json python tools/bench_adjoint.py --size 128 --steps 80
   step "rocprof adjoint 128" 400 $O/prof_adjoint.log rocprofv3 --kernel-trace --stats -d $O/prof_adjoint -o run --output-format csv -- python3 $R/tools/bench_adjoint.py --size 128 --steps 20 ;;
+examples_a) step "reference examples (part a) on the GPU, 100 its" 1100 $O/examples_gpu_a.jsonl python tools/run_examples.py --infer --device cuda --iters 100 --timeout 120 --cwd $R/_refcases --out /tmp/tclb_exa $(cat $R/_refcases/cases_a.txt) ;;
+examples_b) step "reference examples (part b) on the GPU, 100 its" 1100 $O/examples_gpu_b.jsonl python tools/run_examples.py --infer --device cuda --iters 100 --timeout 120 --cwd $R/_refcases --out /tmp/tclb_exb $(cat $R/_refcases/cases_b.txt) ;;
+globms) step "rocprof mixed-shift globals every step" 400 $O/prof_ms_globevery.log rocprofv3 --kernel-trace --stats -d $O/prof_ms_globevery -o run --output-format csv -- python3 $R/bench.py --steps 10 --warmup 2 --glob-every-step --precision mixed-shift ;;
 smoke) step "smoke" 300 $O/smoke.log python -c "import __graft_entry__ as g; g.smoke()" ;;
 bench1) step "bench fp64" 300 $O/bench_fp64.json python bench.py ;;
 esac; done

@@ -57,6 +57,8 @@ class Adjoint:
         self.reverse = bool(lat.model.reverse) and reverse
         self._seeded = bool(list(settings) or list(zonal))
         self._abuf = None             # persistent (aout, ain) buffers of _ad_stage
+        self._dual_buf = None         # GPU: nodes of a stage without a reverse sweep
+        self._dual_count: Dict[int, int] = {}
         self._ctx_bytes = b""
         self._ovf = torch.zeros(1, dtype=torch.int32, device=dev) if lat.is_gpu else None
 
@@ -104,8 +106,12 @@ class Adjoint:
         cover = self._ad_cover.get(si, 0) if self._ctx_dev is not None else 0
         L.reserved0 = cover
         # hand-written reverse sweeps (Model.set_reverse) on the nodes they cover, unless a
-        # setting gradient is asked for (the sweeps push state adjoints only)
-        L.next[5] = 1 if (self.reverse and not self._seeded) else 0
+        # setting gradient is asked for (the sweeps push state adjoints only).  CPU: one
+        # pass, reverse or dual per node; GPU: launch mode 1 (reverse sweeps, recording the
+        # other nodes once) then mode 2 (dual windows over the recorded nodes only), so no
+        # wave mixes the two (executor_ad_hip.hpp)
+        rev = self.reverse and not self._seeded
+        L.next[5] = 1 if rev else 0
         L.stream = lat._stream()
         first = si not in self._ad_cover
         if self._ctx_dev is not None:
@@ -123,20 +129,38 @@ class Adjoint:
         if lat.cuts is not None:
             L.ext[1] = lat.cuts.data_ptr()
             L.next[1] = lat.cuts.numel()
-        self.lib.run(L)
+        if rev and self._ctx_dev is not None:
+            nodes = (L.xhi - L.xlo) * (L.yhi - L.ylo) * (L.zhi - L.zlo)
+            if self._dual_buf is None or self._dual_buf.numel() < nodes + 1:
+                self._dual_buf = torch.zeros(nodes + 1, dtype=torch.int32, device=lat.device)
+            count = self._dual_count.get(si)
+            if count is None:
+                self._dual_buf[0] = 0
+            L.aux = self._dual_buf.data_ptr()
+            L.qcomp = 0 if count is None else 1          # record the dual nodes on the first call
+            self.lib.run(L)
+            if count is None:
+                count = self._dual_count[si] = int(self._dual_buf[0].item())
+            L.next[5], L.qcomp = 2, count
+            if count > 0:
+                self.lib.run(L)
+            elif first:
+                self._ad_cover[si] = -1                   # nothing for the dual windows
+                first = False
+        else:
+            self.lib.run(L)
         if self._ctx_dev is not None:
             if first:
                 c = abi.AdCtx.from_buffer_copy(bytes(self._ctx_dev.cpu().numpy()))
                 w = self.lib.window
-                covered = -(-cover // w) * w if cover > 0 else (w if cover < 0 else self.lib.tangents)
+                covered = -(-cover // w) * w if cover > 0 else self.lib.tangents
                 if c.reserved > covered:
                     # a node read more inputs than the windows covered: the windows partition
                     # the Jacobian columns, so the missing ones are added by the remaining windows
                     L.reserved2, L.reserved0 = covered, 0
                     self.lib.run(L)
                     c = abi.AdCtx.from_buffer_copy(bytes(self._ctx_dev.cpu().numpy()))
-                # -1: no node of this stage needed the dual passes (every node swept in reverse)
-                self._ad_cover[si] = max(cover, c.reserved) if (c.reserved or not L.next[5]) else -1
+                self._ad_cover[si] = max(cover, c.reserved)
                 if c.overflow:
                     raise AdjointError(f"model {lat.model.name}: a node needed more than "
                                        f"{self.lib.tangents} AD tangents")

@@ -119,30 +119,58 @@ namespace exec {
 // scratch at W = 3 (268 B/lane of spills at the default W = 4).  Every node runs the
 // passes of the launch; after the first call of a stage the host covers only the
 // largest input count seen (adjoint.py), not all K.
+//
+// Models with hand-written reverse sweeps (Model.set_reverse) split the work by launch
+// mode (Launch.next[5]) so a wave never mixes the two kinds of node (a 64-wide x row
+// holding one boundary node would otherwise run the whole dual pass):
+//   0  dual passes over the launch box (no reverse sweeps);
+//   1  reverse sweeps over the box; the nodes without one are appended to the dual-node
+//      list in Launch.aux (int: [0] count, then box-linear node indices), recorded while
+//      Launch.qcomp == 0 (the first call of a stage);
+//   2  dual passes over the Launch.qcomp listed nodes (1-D grid).
+// (aux / qcomp are the quantity-launch fields, unused by stage launches.)
 template <class Model, int STG>
 __global__ void __launch_bounds__(AD_BLOCK) k_ad(const Launch L) {
   typedef Dual<double, TCLB_AD_WINDOW> D;
   constexpr int NG = Model::NGLOBALS_;
   constexpr int NSUM = Model::NSUMGLOBALS_;
-  const int x = L.xlo + (int)(blockIdx.x * blockDim.x + threadIdx.x);
-  const int y = L.ylo + (int)blockIdx.y;
-  const int z = L.zlo + (int)blockIdx.z;
+  const int mode = (int)L.next[5];
+  const int w = L.xhi - L.xlo, h = L.yhi - L.ylo;
+  int x, y, z;
+  bool active;
+  if (mode == 2) {
+    const int i = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+    active = i < L.qcomp;
+    const int lin = active ? ((const int*)L.aux)[1 + i] : 0;
+    x = L.xlo + lin % w;
+    y = L.ylo + (lin / w) % h;
+    z = L.zlo + lin / (w * h);
+  } else {
+    x = L.xlo + (int)(blockIdx.x * blockDim.x + threadIdx.x);
+    y = L.ylo + (int)blockIdx.y;
+    z = L.zlo + (int)blockIdx.z;
+    active = x < L.xhi;
+  }
   AdCtx* ctx = (AdCtx*)L.ext[5];
-  int n = 0;
-  bool rev = false;
   if constexpr (has_rev<typename Model::template NodeT<double, double, true>>::value) {
-    // nodes with a hand-written reverse sweep (Model.set_reverse; Launch.next[5] = 1 when
-    // no setting is seeded) run it once, in the first window launch, and skip the dual
-    // passes of every window
-    if (x < L.xhi && L.next[5] == 1) {
-      double gd[NG > 0 ? NG : 1];
-      for (int i = 0; i < NG; i++) gd[i] = 0.0;
-      typename Model::template NodeT<double, double, true> nr(L, x, y, z, gd);
-      rev = nr.template rev_ok<STG>();
-      if (rev && L.reserved2 == 0) nr.template rev_stage<STG>(*ctx);
+    if (mode == 1) {
+      if (active) {
+        double gd[NG > 0 ? NG : 1];
+        for (int i = 0; i < NG; i++) gd[i] = 0.0;
+        typename Model::template NodeT<double, double, true> nr(L, x, y, z, gd);
+        if (nr.template rev_ok<STG>()) {
+          nr.template rev_stage<STG>(*ctx);
+        } else if (L.qcomp == 0) {
+          int* list = (int*)L.aux;
+          const int k = atomicAdd(list, 1);
+          list[1 + k] = (x - L.xlo) + w * ((y - L.ylo) + h * (z - L.zlo));
+        }
+      }
+      return;
     }
   }
-  if (x < L.xhi && !rev) {
+  int n = 0;
+  if (active) {
     D g[NG];
     for (int i = 0; i < NG; i++) g[i] = i < NSUM ? D(0.0) : D(-1e30);
     typename Model::template NodeT<D, double, true> nd(L, x, y, z, g);
@@ -163,11 +191,18 @@ template <class Model, int... I>
 inline int ad_hip_impl(const Launch& L, std::integer_sequence<int, I...>) {
   const int w = L.xhi - L.xlo, h = L.yhi - L.ylo, d = L.zhi - L.zlo;
   if (w <= 0 || h <= 0 || d <= 0) return 0;
-  const dim3 grid((w + AD_BLOCK - 1) / AD_BLOCK, h, d), block(AD_BLOCK, 1, 1);
+  const int mode = (int)L.next[5];
+  dim3 grid((w + AD_BLOCK - 1) / AD_BLOCK, h, d);
+  const dim3 block(AD_BLOCK, 1, 1);
+  if (mode == 2) {
+    if (L.qcomp <= 0) return 0;
+    grid = dim3((L.qcomp + AD_BLOCK - 1) / AD_BLOCK, 1, 1);
+  }
   hipStream_t s = (hipStream_t)L.stream;
-  // windows [L.reserved2, L.reserved0) of the input list (reserved0 = 0: all TCLB_AD_K)
-  // (reserved0 < 0: every node of the stage runs its reverse sweep: one launch)
-  const int end = L.reserved0 < 0 ? 1 : ((L.reserved0 > 0 && L.reserved0 < TCLB_AD_K) ? L.reserved0 : TCLB_AD_K);
+  // windows [L.reserved2, L.reserved0) of the input list (reserved0 = 0: all TCLB_AD_K);
+  // mode 1 (reverse sweeps) is a single launch
+  const int end = mode == 1 ? L.reserved2 + 1
+                            : ((L.reserved0 > 0 && L.reserved0 < TCLB_AD_K) ? L.reserved0 : TCLB_AD_K);
   for (int base = L.reserved2; base < end; base += TCLB_AD_WINDOW) {
     Launch Lb = L;
     Lb.reserved2 = base;
