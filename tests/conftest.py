@@ -17,3 +17,15 @@ def _restore_cwd():
     cwd = os.getcwd()
     yield
     os.chdir(cwd)
+
+
+def _devices():
+    import torch
+    return ["cpu", pytest.param("cuda", marks=[pytest.mark.gpu, pytest.mark.skipif(
+        not torch.cuda.is_available(), reason="no GPU")])]
+
+
+# analytic / physics checks that run on both executors: the CPU one here, the HIP kernels
+# on a GPU box (pytest -m gpu) — independent oracles for the device code, not only
+# HIP-vs-CPU comparisons of the same node source
+DEVICES = _devices()

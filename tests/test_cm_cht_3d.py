@@ -9,11 +9,12 @@ import numpy as np
 import pytest
 import torch
 
+from conftest import DEVICES
 from tclb_amd.lattice import Lattice
 
 
-def _lat(shape, collision="CM", extra=None, model="d3q27q7_cm_cht", **settings):
-    lat = Lattice(model, shape)
+def _lat(shape, collision="CM", extra=None, model="d3q27q7_cm_cht", device="cpu", **settings):
+    lat = Lattice(model, shape, device=torch.device(device))
     m = lat.model
     flags = np.full((lat.NZ, lat.NY, shape[0]), m.node_type(collision).value, dtype=np.uint32)
     if extra is not None:
@@ -28,20 +29,21 @@ def _lat(shape, collision="CM", extra=None, model="d3q27q7_cm_cht", **settings):
 Q27_COLLISIONS = ["CM_HIGHER", "CM_HIGHER_PROB", "CM_HIGHER_PROB_M_EQ", "Cumulants", "Cumulants_HIGHER", "CM", "BGK"]
 
 
+@pytest.mark.parametrize("device", DEVICES)
 @pytest.mark.parametrize("model,collision", [("d3q27q7_cm_cht", c) for c in ("CM", "CM_PROB", "BGK")] +
                          [("d3q27q27_cm_cht", c) for c in Q27_COLLISIONS])
-def test_heat_diffusion(model, collision):
+def test_heat_diffusion(model, collision, device):
     nx, k, steps, a = 32, 0.05, 300, 0.05
-    lat = _lat((nx, 2, 2), collision, model=model, conductivity=k, InitTemperature=1.0, nu=0.1)
+    lat = _lat((nx, 2, 2), collision, model=model, device=device, conductivity=k, InitTemperature=1.0, nu=0.1)
     m = lat.model
     f = lat.fields_interior().clone()
-    x = torch.arange(nx, dtype=f.dtype)
+    x = torch.arange(nx, dtype=f.dtype, device=f.device)
     prof = 1 + a * torch.sin(2 * math.pi * x / nx)
     sel = [i for i, fl in enumerate(m.fields) if fl.group == "h"]
     f[sel] = f[sel] * prof[None, None, None, :]
     lat.set_fields_interior(f)
     lat.iterate(steps)
-    t = lat.quantity("T")[0, 0, 0].double().numpy()
+    t = lat.quantity("T")[0, 0, 0].double().cpu().numpy()
     amp = (t.max() - t.min()) / 2
     kk = 2 * math.pi / nx
     expect = a * math.exp(-k * kk * kk * steps)

@@ -7,6 +7,8 @@ import xml.etree.ElementTree as ET
 import numpy as np
 import pytest
 
+from conftest import DEVICES
+
 from tclb_amd import handlers  # noqa: F401
 from tclb_amd.solver import Solver
 
@@ -73,7 +75,8 @@ def test_kuper_coexistence():
     assert np.abs(lat.quantity("U").numpy()).max() < 5e-3
 
 
-def test_kuper3d_drop():
+@pytest.mark.parametrize("device", DEVICES)
+def test_kuper3d_drop(device):
     """d3q19_kuper (reference models/multiphase/d3q19_kuper): a liquid sphere (R=11) in
     vapour at T=0.65 relaxes to a stable drop at the EOS coexistence densities (liquid
     ~3.05; vapour raised above the flat-interface 0.065 by the Laplace pressure) with
@@ -81,7 +84,7 @@ def test_kuper3d_drop():
     import torch
     from tclb_amd.lattice import Lattice
     n = 32
-    lat = Lattice("d3q19_kuper", (n, n, n), device=torch.device("cpu"), precision="double")
+    lat = Lattice("d3q19_kuper", (n, n, n), device=torch.device(device), precision="double")
     m = lat.model
     zi = lat.add_zone("drop")
     Z, Y, X = np.mgrid[0:n, 0:n, 0:n]
@@ -96,24 +99,25 @@ def test_kuper3d_drop():
     lat.set_setting("Density", 0.04)
     lat.set_setting("Density", 2.9, zone="drop")
     lat.init()
-    m0 = lat.quantity("Rho").numpy().sum()
+    m0 = lat.quantity("Rho").cpu().numpy().sum()
     lat.iterate(500)
-    r = lat.quantity("Rho").numpy()[0]
+    r = lat.quantity("Rho").cpu().numpy()[0]
     assert abs(r[n // 2, n // 2, n // 2] - 3.05) < 0.05
     assert 0.08 < r[2, 2, 2] < 0.14
     assert abs(r.sum() / m0 - 1) < 1e-11
-    assert np.abs(lat.quantity("U").numpy()).max() < 2e-3
+    assert np.abs(lat.quantity("U").cpu().numpy()).max() < 2e-3
 
 
+@pytest.mark.parametrize("device", DEVICES)
 @pytest.mark.parametrize("name", ["d2q9_pf", "d2q9_pf_fd"])
-def test_phase_field_profile(name):
+def test_phase_field_profile(name, device):
     """d2q9_pf (reference models/multiphase/d2q9_pf): a slab of phase +1/2 in -1/2
     relaxes to the conservative Allen-Cahn equilibrium profile 1/2 tanh(2 W x)
     (W = IntWidth), with the phase field conserved."""
     import torch
     from tclb_amd.lattice import Lattice
     n, W = 64, 0.25
-    lat = Lattice(name, (n, 4, 1), device=torch.device("cpu"), precision="double")
+    lat = Lattice(name, (n, 4, 1), device=torch.device(device), precision="double")
     m = lat.model
     zi = lat.add_zone("liq")
     fl = np.full((lat.NZ, lat.NY, n), m.node_type("MRT").value, dtype=np.uint32)
@@ -124,9 +128,9 @@ def test_phase_field_profile(name):
     lat.set_setting("PhaseField", -0.5)
     lat.set_setting("PhaseField", 0.5, zone="liq")
     lat.init()
-    p0 = (lat.quantity("PhaseField").numpy() + 0.5).sum()
+    p0 = (lat.quantity("PhaseField").cpu().numpy() + 0.5).sum()
     lat.iterate(3000)
-    p = lat.quantity("PhaseField").numpy()[0, 0]
+    p = lat.quantity("PhaseField").cpu().numpy()[0, 0]
     x = np.arange(n) + 0.0
     ref = np.where(x < 32, 0.5 * np.tanh(2 * W * (x - 15.5)), -0.5 * np.tanh(2 * W * (x - 47.5)))
     assert np.abs(p - ref[None]).max() < 0.01

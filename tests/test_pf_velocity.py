@@ -4,12 +4,14 @@ MRT, central-moment and BGK collisions; a drop on a wall with a contact angle sp
 (geometric wetting through the wall normals) (reference models/multiphase/d2q9_pf_velocity)."""
 import numpy as np
 import pytest
+import torch
 
+from conftest import DEVICES
 from tclb_amd.lattice import Lattice
 
 
-def _drop(model, coll, n=40, R0=9.0, sigma=0.01, steps=1000, flags=None, **extra):
-    lat = Lattice(model, (n, n, 1))
+def _drop(model, coll, n=40, R0=9.0, sigma=0.01, steps=1000, flags=None, device="cpu", **extra):
+    lat = Lattice(model, (n, n, 1), device=torch.device(device))
     m = lat.model
     fl = np.full((lat.NZ, lat.NY, n), m.node_type(coll).value, dtype=np.uint32) if flags is None else flags(m, lat)
     lat.set_flags(fl)
@@ -26,12 +28,13 @@ def _drop(model, coll, n=40, R0=9.0, sigma=0.01, steps=1000, flags=None, **extra
 
 @pytest.mark.parametrize("model,coll", [("d2q9_pf_velocity", "MRT"), ("d2q9_pf_velocity_CM", "CM"),
                                         ("d2q9_pf_velocity_BGK", "BGK")])
-def test_pf_velocity_static_drop(model, coll):
+@pytest.mark.parametrize("device", DEVICES)
+def test_pf_velocity_static_drop(model, coll, device):
     n, R0, sigma = 40, 9.0, 0.01
-    lat, phi0 = _drop(model, coll, n, R0, sigma)
-    phi = lat.quantity("PhaseField")[0, 0].double().numpy()
-    p = lat.quantity("Pressure")[0, 0].double().numpy()
-    u = lat.quantity("U")[:2].double().numpy()
+    lat, phi0 = _drop(model, coll, n, R0, sigma, device=device)
+    phi = lat.quantity("PhaseField")[0, 0].double().cpu().numpy()
+    p = lat.quantity("Pressure")[0, 0].double().cpu().numpy()
+    u = lat.quantity("U")[:2].double().cpu().numpy()
     assert np.isfinite(p).all()
     assert abs(phi.sum() - phi0) < 1e-8 * phi0
     c = n // 2
