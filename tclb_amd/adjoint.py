@@ -26,6 +26,7 @@ from typing import Dict, List, Optional, Sequence
 import numpy as np
 import torch
 
+from .lattice import _runs
 from .ops import abi
 
 
@@ -56,10 +57,12 @@ class Adjoint:
         # reverse=False forces the dual-number passes everywhere (tests, A/B)
         self.reverse = bool(lat.model.reverse) and reverse
         self._seeded = bool(list(settings) or list(zonal))
-        self._abuf = None             # persistent (aout, ain) buffers of _ad_stage
+        self._abuf = None             # persistent (aout, ain) ping-pong buffers of _ad_stage
         self._dual_buf = None         # GPU: nodes of a stage without a reverse sweep
         self._dual_count: Dict[int, int] = {}
-        self._ctx_bytes = b""
+        self._ctx_bytes = [b"", b""]
+        self._ctx_devs = ([self._ctx_dev, torch.zeros_like(self._ctx_dev)] if self._ctx_dev is not None
+                          else [None, None])
         self._ovf = torch.zeros(1, dtype=torch.int32, device=dev) if lat.is_gpu else None
 
     # ------------------------------------------------------------------ one action
@@ -74,9 +77,15 @@ class Adjoint:
         lat = self.lat
         if self._abuf is None:
             self._abuf = (torch.zeros_like(aout), torch.zeros_like(aout))
-        aout_b, ain = self._abuf
-        if aout is not aout_b:
-            aout_b.copy_(aout)
+        # ping-pong: the output adjoint of one call is the input of the next, so in a sweep
+        # no adjoint snapshot is copied; each parity has its own device AdCtx
+        if aout is self._abuf[1]:
+            par = 1
+        else:
+            par = 0
+            if aout is not self._abuf[0]:
+                self._abuf[0].copy_(aout)
+        aout_b, ain = self._abuf[par], self._abuf[1 - par]
         ain.zero_()
         L = lat._base_launch()
         lat._sync_settings()
@@ -116,10 +125,12 @@ class Adjoint:
         first = si not in self._ad_cover
         if self._ctx_dev is not None:
             raw = bytes(c)
-            if first or raw != self._ctx_bytes:
-                self._ctx_dev.copy_(torch.frombuffer(bytearray(raw), dtype=torch.uint8))
-                self._ctx_bytes = raw
-            L.ext[5] = self._ctx_dev.data_ptr()
+            dev_ctx = self._ctx_devs[par]
+            if first or raw != self._ctx_bytes[par]:
+                dev_ctx.copy_(torch.frombuffer(bytearray(raw), dtype=torch.uint8))
+                self._ctx_bytes[par] = raw
+            self._ctx_dev = dev_ctx
+            L.ext[5] = dev_ctx.data_ptr()
         else:
             L.ext[5] = ctypes.cast(ctypes.pointer(c), ctypes.c_void_p)
         if lat.turb_t is not None:
@@ -172,7 +183,7 @@ class Adjoint:
         elif c.overflow:
             raise AdjointError(f"model {lat.model.name}: a node needed more than {self.lib.tangents} AD tangents")
         lat.reverse_halo(ain)
-        return ain.clone()
+        return ain
 
     def _free_bytes(self) -> float:
         if self.lat.is_gpu:
@@ -191,11 +202,22 @@ class Adjoint:
             raise AdjointError(f"model {self.lat.model.name}: a node needed more than {self.lib.tangents} AD tangents")
 
     def step_back(self, a_next: torch.Tensor, action: str = "Iteration", obj_weight: float = 1.0,
-                  state: Optional[torch.Tensor] = None) -> torch.Tensor:
+                  state: Optional[torch.Tensor] = None, _buffer: bool = False) -> torch.Tensor:
         """adjoint of one `action` applied to the primal state `state` (default: the
         current snapshot): given a_next = dJ/d(state after the action) return
         dJ/d(state before), adding this step's Objective derivative (weight obj_weight)
-        and setting gradients."""
+        and setting gradients.  (_buffer: the result may be one of the adjoint's internal
+        ping-pong buffers, valid until the next call — the unsteady sweep's own loop.)"""
+        a = self._step_back(a_next, action, obj_weight, state)
+        if not _buffer and self._abuf is not None and any(a is b for b in self._abuf):
+            a = a.clone()
+        return a
+
+    def _step_back(self, a_next, action, obj_weight, state):
+        if (len(self.lat.model.action(action).stages) > 1 and self._abuf is not None
+                and any(a_next is b for b in self._abuf)):
+            # a_next is read again after the first stage's adjoint reuses the buffers
+            a_next = a_next.clone()
         lat = self.lat
         m = lat.model
         act = m.action(action)
@@ -219,12 +241,17 @@ class Adjoint:
             st = m.stage(act.stages[k])
             si = m.stage_index(act.stages[k])
             saved = lat._saved_fields(st)
-            aout = torch.zeros_like(a)
-            aout[saved] = a[saved]
+            if len(saved) == a.shape[0]:
+                aout = a                 # every field is an output of the stage
+            else:
+                aout = torch.zeros_like(a)
+                for r0, r1 in _runs(saved):
+                    aout[r0:r1] = a[r0:r1]
             ain = self._ad_stage(si, inputs[k], aout, obj_weight)
             if k > 0:
                 keep = a.clone()
-                keep[saved] = 0          # written in place: the old values are overwritten
+                for r0, r1 in _runs(saved):
+                    keep[r0:r1] = 0      # written in place: the old values are overwritten
                 a = ain + keep
             else:
                 a = ain                  # B's unwritten fields do not depend on A
@@ -267,30 +294,35 @@ class Adjoint:
         bases = sorted(snaps)
         for si, base in reversed(list(enumerate(bases))):
             end = bases[si + 1] if si + 1 < len(bases) else steps
-            # re-run the segment once, keeping the state before every step
+            # re-run the segment once, keeping the state before every step: each step
+            # writes a fresh snapshot buffer, which is kept (no copies)
             lat.snaps[lat.cur].copy_(snaps[base])
             lat.iter = it0 + base
             states = [snaps[base]]
             for t in range(base + 1, end if keep_segment else base + 1):
+                lat.snaps[1 - lat.cur] = lat.new_snapshot()
                 lat.iterate(1, glob_last=False, action=action)
-                states.append(lat.snaps[lat.cur].clone())
+                states.append(lat.snaps[lat.cur])
             for t in range(end - 1, base - 1, -1):
                 if keep_segment:
-                    lat.snaps[lat.cur].copy_(states[t - base])
+                    state = states[t - base]
                 else:
                     lat.snaps[lat.cur].copy_(snaps[base])
                     lat.iter = it0 + base
                     for _ in range(t - base):
                         lat.iterate(1, glob_last=False, action=action)
+                    state = None
                 lat.iter = it0 + t
                 if lat.zseries:
                     lat.apply_series()
                     before = self.gzon.cpu().numpy().copy()
-                a = self.step_back(a, action)
+                a = self.step_back(a, action, state=state, _buffer=True)
                 if lat.zseries:
                     self._series_grad(before, lat)
             del states
         self.check_overflow()
+        a = a.clone()
+        lat.snaps = [lat.new_snapshot(), lat.new_snapshot()]
         lat.snaps[cur_final].copy_(final)
         lat.cur = cur_final
         lat.iter = it0 + steps

@@ -115,9 +115,7 @@ class Lattice:
         self.fs = plane + self.field_pad
         if self.fs >= 2 ** 31:
             raise ValueError("local field exceeds 2^31 elements; use more ranks")
-        self.snaps = [torch.zeros(nf * self.fs, dtype=self.sdtype, device=self.device)
-                      .as_strided((nf, self.NZ, self.NY, self.px), (self.fs, self.NY * self.px, self.px, 1))
-                      for _ in range(2)]
+        self.snaps = [self.new_snapshot() for _ in range(2)]
         self.cur = 0
         fdt = torch.int16 if m.flag_bits == 16 else torch.int32
         self.flags = torch.zeros((self.NZ, self.NY, self.px), dtype=fdt, device=self.device)
@@ -169,6 +167,12 @@ class Lattice:
         self.cuts = None
         self.particles = None     # ParticleSystem with pre_stage/post_stage/step hooks
         self.average_start = 0
+
+    def new_snapshot(self) -> torch.Tensor:
+        """a zeroed snapshot buffer with the layout of snaps[0/1] ([nf][NZ][NY][px], field
+        stride fs): the A/B pair, and states kept by the adjoint's checkpointing"""
+        return (torch.zeros(self.nf * self.fs, dtype=self.sdtype, device=self.device)
+                .as_strided((self.nf, self.NZ, self.NY, self.px), (self.fs, self.NY * self.px, self.px, 1)))
 
     # ------------------------------------------------------------------ launch
     def _base_launch(self) -> abi.Launch:
