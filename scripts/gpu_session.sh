@@ -83,4 +83,14 @@ examples_b) step "reference examples (part b) on the GPU, 100 its" 1100 $O/examp
 globms) step "rocprof mixed-shift globals every step" 400 $O/prof_ms_globevery.log rocprofv3 --kernel-trace --stats -d $O/prof_ms_globevery -o run --output-format csv -- python3 $R/bench.py --steps 10 --warmup 2 --glob-every-step --precision mixed-shift ;;
 smoke) step "smoke" 300 $O/smoke.log python -c "import __graft_entry__ as g; g.smoke()" ;;
 bench1) step "bench fp64" 300 $O/bench_fp64.json python bench.py ;;
+r03i)
+  step "part256 grid container" 300 $O/part256_grid.log python tools/bench_configs.py --configs part256
+  step "part256 tree container" 300 $O/part256_tree.log env TCLB_SOLID_CONTAINER=tree python tools/bench_configs.py --configs part256
+  step "pf384 mixed-shift, scalar zonal reads" 300 $O/pf384_ms_a.log python tools/bench_configs.py --configs pf384 --precision mixed-shift
+  step "pf384 mixed-shift, vector zonal reads" 300 $O/pf384_ms_zvec_a.log env TCLB_VARIANT=zvec python tools/bench_configs.py --configs pf384 --precision mixed-shift
+  step "pf384 mixed-shift, scalar zonal reads (2)" 300 $O/pf384_ms_b.log python tools/bench_configs.py --configs pf384 --precision mixed-shift
+  step "pf384 mixed-shift, vector zonal reads (2)" 300 $O/pf384_ms_zvec_b.log env TCLB_VARIANT=zvec python tools/bench_configs.py --configs pf384 --precision mixed-shift
+  step "pf384 fp64 + globals every step" 300 $O/pf384_fp64_glob.log bash -c 'python tools/bench_configs.py --configs pf384 && python tools/bench_configs.py --configs pf384 --glob-every-step'
+  step "pf384 mixed-shift globals every step" 300 $O/pf384_ms_glob.log python tools/bench_configs.py --configs pf384 --precision mixed-shift --glob-every-step
+  step "d3q27 bench fp64 / globals every step" 400 $O/bench_glob.log bash -c 'python bench.py --steps 50 && python bench.py --steps 50 --glob-every-step && python bench.py --steps 50 --precision mixed-shift && python bench.py --steps 50 --precision mixed-shift --glob-every-step' ;;
 esac; done

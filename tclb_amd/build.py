@@ -39,6 +39,8 @@ VARIANTS = {
     # occupancy floor for the fp32/fp16-storage kernels (executor_hip.hpp k_stage_narrow)
     "nw3": ["-DTCLB_NT_STORE=1", "-DTCLB_NARROW_WAVES=3"],
     "nw4": ["-DTCLB_NT_STORE=1", "-DTCLB_NARROW_WAVES=4"],
+    # zonal settings read with plain per-lane vector loads (core.hpp zonal_read A/B)
+    "zvec": ["-DTCLB_NT_STORE=1", "-DTCLB_ZONAL_SCALAR=0"],
 }
 DEFAULT_VARIANT = os.environ.get("TCLB_VARIANT", "")
 # CPU executor variants: "ubsan" builds the node code with UndefinedBehaviorSanitizer
@@ -309,13 +311,13 @@ def _write_src_stamp(name: str, kind: str, variant: str, s: Optional[str] = None
 
 
 def build_host(force: bool = False, verbose: bool = False) -> str:
-    """native host runtime library (geometry voxeliser, scans, HDF5 writer): libtclb_host.so
+    """native host runtime library (geometry voxeliser, scans, HDF5 and PNG writers): libtclb_host.so
     from every csrc/runtime/*.cpp"""
     rdir = os.path.join(CSRC, "runtime")
     srcs = sorted(os.path.join(rdir, f) for f in os.listdir(rdir) if f.endswith(".cpp"))
     target = os.path.join(LIB, "libtclb_host.so")
     os.makedirs(LIB, exist_ok=True)
-    cmd = [CXX, "-O3", "-std=c++17", "-fPIC", "-shared", "-fopenmp", *srcs, "-o", target + ".tmp"]
+    cmd = [CXX, "-O3", "-std=c++17", "-fPIC", "-shared", "-fopenmp", *srcs, "-lz", "-o", target + ".tmp"]
     h = _hash_inputs(srcs, " ".join(cmd))
     stamp = target + ".hash"
     if not force and os.path.exists(target) and os.path.exists(stamp) and open(stamp).read() == h:

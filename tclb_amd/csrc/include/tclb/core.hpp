@@ -43,6 +43,9 @@ struct vec3 {
 // Layout of one snapshot: storage_t[nfields][nz+2gz][ny+2gy][px], x fastest (SoA, like
 // the reference's field-major margin blocks, src/conf.R:952-957) but with contiguous
 // ghost planes on the decomposed axis instead of 27 margin blocks.
+// Launch.glob bit: no zone has a nonzero objective weight (<global>InObj), so AddTo<global>
+// skips the weighted Objective sum and its per-node zonal-table reads (a scalar branch).
+#define TCLB_GLOB_NOOBJ 4
 struct Launch {
   const void* in;          // input snapshot base
   void* out;               // output snapshot base
@@ -61,7 +64,8 @@ struct Launch {
   int iter;                // iteration counter (Time)
   int nzones;              // zone pitch of the zonal table
   int stage;               // stage index (see model meta)
-  int glob;                // 0: no globals, 1: integrate globals
+  int glob;                // bit 0: integrate globals; bit 2 (TCLB_GLOB_NOOBJ): every
+                           // <global>InObj weight is zero, the Objective sum is skipped
   int quantity;            // quantity index for get-quantity launches
   int qcomp;               // component stride of vector quantities (elements)
   double qscale;           // unit scale for quantity output
@@ -86,6 +90,35 @@ struct Launch {
   int moy, moz;
   signed char mslot[TCLB_MIRROR_FIELDS];
 };
+
+// Zonal-table read (reference ZoneSettings, one value per zone): the zone comes from the
+// node's flags, so a plain indexed load is a per-lane vector load that each use waits on
+// (seen as chains of global_load_dwordx2 + s_waitcnt vmcnt(0) in the pf_velocity
+// collision).  On the GPU the value of the zone of the wave's first lane is fetched by a
+// scalar load (s_load: constant cache, short latency; a read, the table is never written
+// by a kernel); only lanes of another zone issue the vector load, and a wave with a single
+// zone (nearly all of them) skips it.  -DTCLB_ZONAL_SCALAR=0 (build variant "zvec") keeps
+// the plain load for A/B runs.
+#ifndef TCLB_ZONAL_SCALAR
+#define TCLB_ZONAL_SCALAR 1
+#endif
+TCLB_FN double zonal_read(const Launch& L, int k, int zone) {
+#if TCLB_GPU && defined(__HIP_DEVICE_COMPILE__) && TCLB_ZONAL_SCALAR
+  const int z0 = __builtin_amdgcn_readfirstlane(zone);
+  // the address is wave-uniform by construction (k is a constant of the emitted accessor,
+  // z0 and L are uniform); readfirstlane of its halves lets the backend keep it in SGPRs
+  // where its divergence analysis cannot tell (e.g. inside the AD node)
+  const unsigned long long a = (unsigned long long)(L.zonal + ((long long)k * L.nzones + z0));
+  const unsigned long long au = (unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)a) |
+                                ((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)(a >> 32)) << 32);
+  double r;
+  asm("s_load_dwordx2 %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(r) : "s"(au));
+  if (zone != z0) r = L.zonal[(long long)k * L.nzones + zone];
+  return r;
+#else
+  return L.zonal[(long long)k * L.nzones + zone];
+#endif
+}
 
 template <class S>
 TCLB_FN void mirror_store(const Launch& L, int fi, int x, int y, int z, S v) {
@@ -311,12 +344,13 @@ inline int iterate_action(Launch L, int nsteps, const int* stages, int nstages, 
                           const SamplePlan* sp, Run run, Sample sample) {
   const void* cur = L.in;
   void* nxt = L.out;
+  const int gflags = L.glob & ~1;
   for (int s = 0; s < nsteps; s++) {
     for (int k = 0; k < nstages; k++) {
       L.in = k == 0 ? cur : nxt;
       L.out = nxt;
       L.stage = stages[k];
-      L.glob = (glob_last && s == nsteps - 1) ? 1 : 0;
+      L.glob = (glob_last && s == nsteps - 1) ? (1 | gflags) : 0;
       const int r = run(L);
       if (r != 0) return r;
     }

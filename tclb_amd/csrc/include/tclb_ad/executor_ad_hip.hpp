@@ -124,11 +124,36 @@ namespace exec {
 // mode (Launch.next[5]) so a wave never mixes the two kinds of node (a 64-wide x row
 // holding one boundary node would otherwise run the whole dual pass):
 //   0  dual passes over the launch box (no reverse sweeps);
-//   1  reverse sweeps over the box; the nodes without one are appended to the dual-node
-//      list in Launch.aux (int: [0] count, then box-linear node indices), recorded while
-//      Launch.qcomp == 0 (the first call of a stage);
-//   2  dual passes over the Launch.qcomp listed nodes (1-D grid).
+//   1  reverse sweeps over the box (kernel k_rev, its own register budget: the dual
+//      path's would cut its occupancy to one wave); the nodes without one are appended to
+//      the dual-node list in Launch.aux (int: [0] count, then box-linear node indices),
+//      recorded while Launch.qcomp == 0 (the first call of a stage);
+//   2  dual passes over the Launch.qcomp listed nodes, every window in one launch
+//      (grid.y = window: a few boundary planes of nodes alone cannot fill the GPU).
 // (aux / qcomp are the quantity-launch fields, unused by stage launches.)
+template <class Model, int STG>
+__global__ void __launch_bounds__(256) k_rev(const Launch L) {
+  constexpr int NG = Model::NGLOBALS_;
+  const int x = L.xlo + (int)(blockIdx.x * blockDim.x + threadIdx.x);
+  const int y = L.ylo + (int)(blockIdx.y * blockDim.y + threadIdx.y);
+  const int z = L.zlo + (int)blockIdx.z;
+  if (x >= L.xhi || y >= L.yhi) return;
+  if constexpr (has_rev<typename Model::template NodeT<double, double, true>>::value) {
+    AdCtx* ctx = (AdCtx*)L.ext[5];
+    double gd[NG > 0 ? NG : 1];
+    for (int i = 0; i < NG; i++) gd[i] = 0.0;
+    typename Model::template NodeT<double, double, true> nr(L, x, y, z, gd);
+    if (nr.template rev_ok<STG>()) {
+      nr.template rev_stage<STG>(*ctx);
+    } else if (L.qcomp == 0) {
+      const int w = L.xhi - L.xlo, h = L.yhi - L.ylo;
+      int* list = (int*)L.aux;
+      const int k = atomicAdd(list, 1);
+      list[1 + k] = (x - L.xlo) + w * ((y - L.ylo) + h * (z - L.zlo));
+    }
+  }
+}
+
 template <class Model, int STG>
 __global__ void __launch_bounds__(AD_BLOCK) k_ad(const Launch L) {
   typedef Dual<double, TCLB_AD_WINDOW> D;
@@ -152,28 +177,15 @@ __global__ void __launch_bounds__(AD_BLOCK) k_ad(const Launch L) {
     active = x < L.xhi;
   }
   AdCtx* ctx = (AdCtx*)L.ext[5];
-  if constexpr (has_rev<typename Model::template NodeT<double, double, true>>::value) {
-    if (mode == 1) {
-      if (active) {
-        double gd[NG > 0 ? NG : 1];
-        for (int i = 0; i < NG; i++) gd[i] = 0.0;
-        typename Model::template NodeT<double, double, true> nr(L, x, y, z, gd);
-        if (nr.template rev_ok<STG>()) {
-          nr.template rev_stage<STG>(*ctx);
-        } else if (L.qcomp == 0) {
-          int* list = (int*)L.aux;
-          const int k = atomicAdd(list, 1);
-          list[1 + k] = (x - L.xlo) + w * ((y - L.ylo) + h * (z - L.zlo));
-        }
-      }
-      return;
-    }
-  }
+  // mode 2: window of this block row (no setting is seeded in mode 2, so the window base
+  // can be set after the node constructor, before its loads seed the inputs)
+  const int wbase = mode == 2 ? L.reserved2 + (int)blockIdx.y * TCLB_AD_WINDOW : L.reserved2;
   int n = 0;
   if (active) {
     D g[NG];
     for (int i = 0; i < NG; i++) g[i] = i < NSUM ? D(0.0) : D(-1e30);
     typename Model::template NodeT<D, double, true> nd(L, x, y, z, g);
+    nd.ad_.base = wbase;
     nd.template run_stage<STG>();
     if (ctx->obj_weight != 0.0) nd.ad_.scatter(ctx->obj_weight, g[Model::OBJ_]);
     nd.ad_.flush();
@@ -181,7 +193,7 @@ __global__ void __launch_bounds__(AD_BLOCK) k_ad(const Launch L) {
   }
   // first pass: the largest input count of the launch (ctx->reserved), from which the
   // host sizes the passes of later calls of this stage (AdCtx.reserved, adjoint.py)
-  if (L.reserved2 == 0) {
+  if (wbase == 0) {
     for (int off = AD_BLOCK / 2; off > 0; off >>= 1) n = max(n, __shfl_xor(n, off));
     if (threadIdx.x == 0 && n > 0) atomicMax(&ctx->reserved, n);
   }
@@ -194,15 +206,25 @@ inline int ad_hip_impl(const Launch& L, std::integer_sequence<int, I...>) {
   const int mode = (int)L.next[5];
   dim3 grid((w + AD_BLOCK - 1) / AD_BLOCK, h, d);
   const dim3 block(AD_BLOCK, 1, 1);
-  if (mode == 2) {
-    if (L.qcomp <= 0) return 0;
-    grid = dim3((L.qcomp + AD_BLOCK - 1) / AD_BLOCK, 1, 1);
-  }
   hipStream_t s = (hipStream_t)L.stream;
-  // windows [L.reserved2, L.reserved0) of the input list (reserved0 = 0: all TCLB_AD_K);
-  // mode 1 (reverse sweeps) is a single launch
-  const int end = mode == 1 ? L.reserved2 + 1
-                            : ((L.reserved0 > 0 && L.reserved0 < TCLB_AD_K) ? L.reserved0 : TCLB_AD_K);
+  // windows [L.reserved2, L.reserved0) of the input list (reserved0 = 0: all TCLB_AD_K)
+  const int end = (L.reserved0 > 0 && L.reserved0 < TCLB_AD_K) ? L.reserved0 : TCLB_AD_K;
+  if (mode == 1) {            // reverse sweeps: one launch, stage-kernel block shape
+    const int bx = w >= 128 ? 128 : 64, by = 256 / bx;
+    const dim3 rgrid((w + bx - 1) / bx, (h + by - 1) / by, d), rblock(bx, by, 1);
+    bool found = false;
+    ((L.stage == I ? (k_rev<Model, I><<<rgrid, rblock, 0, s>>>(L), found = true) : false), ...);
+    return found ? (int)hipGetLastError() : -2;
+  }
+  if (mode == 2) {            // listed nodes, every window in one launch
+    if (L.qcomp <= 0) return 0;
+    const int nwin = (end - L.reserved2 + TCLB_AD_WINDOW - 1) / TCLB_AD_WINDOW;
+    if (nwin <= 0) return 0;
+    grid = dim3((L.qcomp + AD_BLOCK - 1) / AD_BLOCK, nwin, 1);
+    bool found = false;
+    ((L.stage == I ? (k_ad<Model, I><<<grid, block, 0, s>>>(L), found = true) : false), ...);
+    return found ? (int)hipGetLastError() : -2;
+  }
   for (int base = L.reserved2; base < end; base += TCLB_AD_WINDOW) {
     Launch Lb = L;
     Lb.reserved2 = base;

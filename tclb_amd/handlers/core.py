@@ -293,6 +293,25 @@ class Catalyst(Callback):
         return self.solver.write_vtk(self.node.get("name", "Catalyst"), ["all"], self.reg)
 
 
+@register("Graphics")
+class Graphics(Callback):
+    """colour frames (PNG) of a z slice every ``Iterations``: the headless counterpart of
+    the reference's GLUT window (built with GRAPHICS, src/gpu_anim.h, which shows the
+    model's Color() of the middle slice, src/LatticeContainer.inc.cpp.Rt:350-423).
+    Attributes: ``name`` (file tag, default Graphics), ``z`` (slice, default middle)."""
+
+    def init(self):
+        super().init()
+        self.name = self.node.get("name", "Graphics")
+        z = self.node.get("z")
+        self.z = None if z is None else int(round(self.solver.units.alt(z)))
+        return 0
+
+    def do_it(self):
+        self.solver.write_frame(self.name, self.z)
+        return 0
+
+
 @register("TXT")
 class TXT(Callback):
     def init(self):

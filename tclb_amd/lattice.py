@@ -132,6 +132,7 @@ class Lattice:
         # (setting index, zone index) -> values; entry (iter % len) is active in an iteration
         self.zseries: Dict[tuple, np.ndarray] = {}
         self._settings_dirty = True
+        self._glob_flags = 0
         self.settings_t = torch.zeros(self.svals.shape, dtype=torch.float64, device=self.device)
         self.zonal_t = torch.zeros(self.zvals.size, dtype=torch.float64, device=self.device)
         # globals accumulator: GSLOTS slots of gstride(NG) doubles (core.hpp TCLB_GSLOTS);
@@ -198,6 +199,9 @@ class Lattice:
             z = np.concatenate([self.zvals.reshape(-1), self.zdt.reshape(-1)])
             self.zonal_t = torch.as_tensor(z, dtype=torch.float64).to(self.device)
             self._settings_dirty = False
+            # no objective weight anywhere: the kernels skip the weighted Objective sum
+            obj = [i for i, n in enumerate(self.zsettings) if n.endswith("InObj")]
+            self._glob_flags = 4 if not np.any(self.zvals[obj]) else 0     # TCLB_GLOB_NOOBJ
         L = self._L
         L.settings = self.settings_t.data_ptr()
         L.zonal = self.zonal_t.data_ptr()
@@ -222,7 +226,7 @@ class Lattice:
         L.in_ = src.data_ptr()
         L.out = dst.data_ptr()
         L.stage = stage
-        L.glob = 1 if glob else 0
+        L.glob = (1 | self._glob_flags) if glob else 0
         L.iter = self.iter
         L.reserved1 = self.iter - self.average_start + 1
         L.stream = self._stream()
@@ -604,6 +608,7 @@ class Lattice:
             L.iter = self.iter
             L.reserved1 = self.iter - self.average_start + 1
             L.stream = self._stream()
+            L.glob = self._glob_flags            # bit 0 set per step by iterate_action
             smp = self.samplers[0] if self.samplers else None
             with trace.span(f"iterate {action} x{n}"):
                 self.lib.iterate(L, self.prec, n, stages, glob_last, smp.plan_for(n) if smp else None)
@@ -822,6 +827,64 @@ class Lattice:
                 self.particles.detach(self)
         L.reserved0 = 0
         return out
+
+    def color(self, z: Optional[int] = None) -> Optional[torch.Tensor]:
+        """the model's node colour pair (value l, weight w; reference ``Color()``) over the
+        global z slice `z` (default: the middle one, reference LatticeContainer::Color):
+        (ny, nx, 2) on this rank's rows, or None when the slice is not on this rank.
+        Evaluated by the quantity kernel with quantity index -1 (the emitted ``color()``)"""
+        gz = self.gshape[2] // 2 if z is None else int(z)
+        if not 0 <= gz < self.gshape[2]:
+            raise ValueError(f"slice z={gz} outside the lattice")
+        lz = gz - self.slab.offset[2]
+        nx, ny, nz = self.shape
+        if not 0 <= lz < nz:
+            return None
+        out = torch.empty((2, ny, nx), dtype=self.rdtype, device=self.device)
+        self._sync_settings()
+        L = self._L
+        L.in_ = self.snaps[self.cur].data_ptr()
+        L.out = self.snaps[1 - self.cur].data_ptr()
+        L.aux = out.data_ptr()
+        L.quantity = -1
+        L.qcomp = nx * ny
+        L.qscale = 1.0
+        L.qsy = nx
+        L.qsz = nx * ny
+        L.reserved0 = 2
+        L.ylo, L.yhi, L.zlo, L.zhi = 0, ny, lz, lz + 1
+        L.iter = self.iter
+        L.reserved1 = max(1, self.iter - self.average_start)
+        L.stream = self._stream()
+        if self.particles is not None:
+            self.particles.attach_for_quantity(self)
+        try:
+            self.lib.quantity(L, self.prec)
+        finally:
+            if self.particles is not None:
+                self.particles.detach(self)
+            L.reserved0 = 0
+            L.zlo, L.zhi = 0, nz
+        return out.permute(1, 2, 0)
+
+    def draw_wall(self, x: int, y: int, z: Optional[int] = None, kind: str = "Wall"):
+        """set one node (global coordinates; z default: the rendered middle slice) to a
+        boundary type — the reference window's mouse editing (MouseMove,
+        src/Solver.cpp.Rt:730-745: FlagOverwrite of NODE_Wall under the pointer)"""
+        m = self.model
+        nt = m.node_type(kind)
+        z = self.gshape[2] // 2 if z is None else int(z)
+        ox, oy, oz = self.slab.offset
+        nx, ny, nz = self.shape
+        lx, ly, lz = int(x) - ox, int(y) - oy, z - oz
+        if not (0 <= lx < nx and 0 <= ly < ny and 0 <= lz < nz):
+            return
+        if nt is None:
+            raise KeyError(f"model {m.name} has no node type {kind}")
+        full = self.flags.cpu().numpy().view(np.uint16 if m.flag_bits == 16 else np.uint32)[:, :, :nx].copy()
+        v = int(full[self.gz + lz, self.gy + ly, lx])
+        full[self.gz + lz, self.gy + ly, lx] = (v & ~nt.mask) | nt.value     # its group only
+        self.set_flags(full)
 
     def _adjoint_quantity(self, q, nc: int) -> torch.Tensor:
         """adjoint quantities (reference AddQuantity(adjoint=T)) from the adjoint state of

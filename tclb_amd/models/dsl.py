@@ -105,6 +105,8 @@ class Stage:
     snapshot_reads: bool = False   # reads of its own saved fields see the pre-stage values
     particle: bool = False
     init: bool = False                        # "Init" stream: no load before main
+    lazy_load: bool = False   # the declared loads are not made before main: main calls
+                              # load_<name>() where it needs them (declared for the halo)
 
 
 @dataclass
@@ -270,9 +272,11 @@ class Model:
     def add_stage(self, name: str, main: Optional[str] = None, load_densities=False,
                   save_fields=False, read_fields: Optional[Sequence[str]] = None,
                   fixed_point: bool = False, particle: bool = False, init: bool = False,
-                  snapshot_reads: bool = False):
+                  snapshot_reads: bool = False, lazy_load: bool = False):
         """AddStage (src/conf.R:295-330): load_densities / save_fields are True (all), False
-        (none) or lists of field names / group tags (reference defaults: FALSE)."""
+        (none) or lists of field names / group tags (reference defaults: FALSE).
+        lazy_load: the stage's main pulls its densities itself (load_<name>()), e.g. only
+        on the nodes a particle covers; the loads still count for halos and hazards."""
         if save_fields is True:
             save_fields = None
         elif save_fields is False:
@@ -280,7 +284,8 @@ class Model:
         st = Stage(name=name, main=main or name, load_densities=load_densities,
                    save_fields=list(save_fields) if save_fields is not None else None,
                    read_fields=list(read_fields) if read_fields is not None else None,
-                   fixed_point=fixed_point, particle=particle, init=init, snapshot_reads=snapshot_reads)
+                   fixed_point=fixed_point, particle=particle, init=init, snapshot_reads=snapshot_reads,
+                   lazy_load=lazy_load)
         self.stages = [s for s in self.stages if s.name != name] + [st]
         return st
 

@@ -95,7 +95,9 @@ def build(q19: bool = False, part: bool = False, coll: str = "MRT", fmt: bool = 
     if part:
         m.add_stage("BaseIteration", "Run", save_fields=["f"], load_densities=["f", "Force"])
         m.add_stage("BaseInit", "Init", save_fields=["f", "Force"])
-        m.add_stage("CalcF", "CalcF", save_fields=["Force"], load_densities=["f"], particle=True)
+        # the densities are pulled only on the nodes a particle covers (auto.inc CalcF)
+        m.add_stage("CalcF", "CalcF", save_fields=["Force"], load_densities=["f"], particle=True,
+                    lazy_load=True)
         m.add_action("Iteration", ["BaseIteration", "CalcF"])
         m.add_action("Init", ["BaseInit", "CalcF"])
     for n in ["EPressure", "EVelocity", "Wall", "WPressure", "WVelocity"]:

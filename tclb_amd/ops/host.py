@@ -34,6 +34,8 @@ def lib():
             L.tclb_nan_scan_f64.restype = ctypes.c_longlong
             L.tclb_nan_scan_f32.argtypes = [P, ctypes.c_longlong]
             L.tclb_nan_scan_f32.restype = ctypes.c_longlong
+            L.tclb_png_write.argtypes = [ctypes.c_char_p, P, i, i]
+            L.tclb_png_write.restype = i
             _lib = L
     return _lib
 
@@ -99,3 +101,12 @@ def h5_create(path: str, datasets) -> list:
     if r < 0:
         raise OSError(f"cannot write {path}")
     return [int(v) for v in off[:n]]
+
+
+def png_write(path: str, rgba: np.ndarray):
+    """write an (h, w, 4) uint8 RGBA image, top row first, as PNG (csrc/runtime/png.cpp)"""
+    a = np.ascontiguousarray(rgba, dtype=np.uint8)
+    if a.ndim != 3 or a.shape[2] != 4:
+        raise ValueError("png_write expects an (h, w, 4) uint8 array")
+    if lib().tclb_png_write(path.encode(), a.ctypes.data, a.shape[1], a.shape[0]) != 0:
+        raise OSError(f"cannot write {path}")

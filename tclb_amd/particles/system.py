@@ -4,7 +4,7 @@ src/RemoteForceInterface.*, src/SolidGrid.h).
 Device-resident design: once attached to a lattice the particle records live on the
 lattice's device — ``P`` (n, 10: position, velocity, angular velocity, radius), the
 force/moment accumulator ``acc`` (n, 6) that the particle stage kernels add into, the
-uniform-grid solid container, and (SimplePart) the rigid-body integration.  A time step
+solid container (a uniform grid, a bounding-volume tree, or none: ``container``), and (SimplePart) the rigid-body integration.  A time step
 therefore issues only device work: zero ``acc`` -> particle stage kernel -> all-reduce of
 ``acc`` over the ranks (RCCL: asynchronous, no host round trip) -> integration kernel.
 The host copies (``x``, ``v``, ``omega``, ``force``, ``torque``) are refreshed lazily,
@@ -59,7 +59,12 @@ class ParticleSystem:
         self._dev_stale = True        # device copy older than the host arrays
         self._d = None                # device tensors (P, acc, qacc, m, free, grid)
         self._dev_key = None
-        self.grid_min = 16            # particles; below this every node scans the full list
+        self.grid_min = 16            # particles; below this the grid is skipped (full scan)
+        # solid container (reference --with-solid-container=grid|tree|all,
+        # src/configure.ac:92-716): chosen at run time here
+        self.container = os.environ.get("TCLB_SOLID_CONTAINER", "grid")
+        if self.container not in ("grid", "tree", "all"):
+            raise ValueError(f"TCLB_SOLID_CONTAINER={self.container!r}: expected grid, tree or all")
 
     @property
     def n(self) -> int:
@@ -93,8 +98,15 @@ class ParticleSystem:
              "qacc": torch.zeros((max(1, n), 6), dtype=torch.float64, device=dev),
              "m": torch.as_tensor(np.where(h["m"] > 0, h["m"], 1.0) if n else np.ones(1)).to(dev),
              "free": torch.as_tensor(~h["fixed"] if n else np.zeros(1, dtype=bool)).to(dev)}
-        d["grid"], d["cell"] = None, 1
-        if n >= self.grid_min:
+        d["grid"], d["cell"], d["kind"] = None, 1, None
+        if self.container == "tree" and n >= 1:
+            nl = 1 << (n - 1).bit_length()
+            d["kind"], d["nl"] = "tree", nl
+            d["grid"] = torch.zeros(8 + nl + 6 * (2 * nl - 1), dtype=torch.int32, device=dev)
+            d["grid"][:8] = torch.tensor([0, 0, 0, 0, 1, nl, 0, 0], dtype=torch.int32)
+            d["mscale"] = 1023.0 / max(1, max(lat.gshape))
+        elif self.container == "grid" and n >= self.grid_min:
+            d["kind"] = "grid"
             d["cell"] = int(np.ceil(h["r"].max() + 2.0))
             gx, gy, gz = (-(-s // d["cell"]) for s in lat.gshape)
             d["ncell"] = gx * gy * gz
@@ -140,6 +152,46 @@ class ParticleSystem:
         g[8:9 + d["ncell"]] = torch.cumsum(cnt, 0).to(torch.int32)
         g[9 + d["ncell"]:] = torch.sort(cid, stable=True).indices.to(torch.int32)
 
+    @staticmethod
+    def _spread10(v):
+        """interleave the 10 low bits of v with two zero bits each (Morton code)"""
+        v = (v | (v << 16)) & 0x030000FF
+        v = (v | (v << 8)) & 0x0300F00F
+        v = (v | (v << 4)) & 0x030C30C3
+        return (v | (v << 2)) & 0x09249249
+
+    def _build_tree(self):
+        """bounding-volume tree solid container on the device (the role of the reference
+        SolidTree, src/SolidTree.hpp:11-120, a kd-tree built on the host): the particles
+        sorted by the Morton code of their centre are the leaves of an implicit complete
+        binary tree (node i has children 2i+1, 2i+2; nl leaves, a power of two, unused
+        ones empty); every node holds the fp32 box of its cut-off spheres (rad + 2, widened
+        by 0.05 so fp32 rounding never drops a candidate), reduced level by level.
+        Layout: int header[8] (kind 1 in [4], nl in [5]), leaf ids[nl] (-1: empty), float
+        boxes[2 nl - 1][6] (lo xyz, hi xyz).  No host round trip."""
+        d, n, nl = self._d, self.n, self._d["nl"]
+        g = d["grid"]
+        P = d["P"][:n]
+        q = (P[:, 0:3] * d["mscale"]).clamp(0, 1023).to(torch.int64)
+        code = self._spread10(q[:, 0]) | (self._spread10(q[:, 1]) << 1) | (self._spread10(q[:, 2]) << 2)
+        order = torch.argsort(code, stable=True)
+        g[8:8 + nl] = -1
+        g[8:8 + n] = order.to(torch.int32)
+        B = g[8 + nl:].view(torch.float32).view(2 * nl - 1, 6)
+        Ps = P[order]
+        cut = (Ps[:, 9] + 2.05)[:, None]
+        B[nl - 1:nl - 1 + n, 0:3] = (Ps[:, 0:3] - cut).to(torch.float32)
+        B[nl - 1:nl - 1 + n, 3:6] = (Ps[:, 0:3] + cut).to(torch.float32)
+        B[nl - 1 + n:, 0:3] = float("inf")
+        B[nl - 1 + n:, 3:6] = float("-inf")
+        lvl = nl.bit_length() - 2          # deepest internal level
+        while lvl >= 0:
+            st, cnt = (1 << lvl) - 1, 1 << lvl
+            ch = B[2 * st + 1:2 * st + 1 + 2 * cnt].view(cnt, 2, 6)
+            B[st:st + cnt, 0:3] = ch[:, :, 0:3].amin(1)
+            B[st:st + cnt, 3:6] = ch[:, :, 3:6].amax(1)
+            lvl -= 1
+
     def _attach(self, lat, acc):
         d = self._d
         L = lat._L
@@ -147,7 +199,7 @@ class ParticleSystem:
         L.ext[3] = acc.data_ptr()
         L.next[2] = self.n
         if d["grid"] is not None:
-            self._build_grid()
+            self._build_tree() if d["kind"] == "tree" else self._build_grid()
             L.ext[4] = d["grid"].data_ptr()
             L.next[4] = d["grid"].numel()
         else:

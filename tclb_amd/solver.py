@@ -237,6 +237,16 @@ class Solver:
                     fields.append((q.name, a[0], 1))
         return fields
 
+    def write_frame(self, name: str = "Graphics", z: Optional[int] = None) -> str:
+        """colour frame of a z slice as PNG (io/render.py; the headless counterpart of the
+        reference's GLUT window): <out>_<name>_<iter>.png, written by the root rank"""
+        from .io import render
+        fn = self.out_iter_collective_file(name, ".png")
+        if self.rank == 0:
+            log.output(f"{self.iter:8d} it writing frame {fn}")
+        render.write_png(self.lattice, fn, z)
+        return fn
+
     def write_vtk(self, name: str, what: Optional[Sequence[str]], region=None):
         from .io import vtk
         lat = self.lattice

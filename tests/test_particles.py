@@ -68,13 +68,14 @@ def test_psm_momentum_balance(name):
     assert abs(lat.globals["TotalFluidMass"] / n ** 3 - 1) < 1e-12
 
 
-def _many(device, grid_min, n=24, count=30):
+def _many(device, grid_min, n=24, count=30, container="grid"):
     lat = Lattice("d3q27_PSM_NEBB", (n, n, n), device=torch.device(device))
     lat.set_flags(np.full((lat.NZ, lat.NY, n), lat.model.node_type("BGK").value, dtype=np.uint32))
     lat.set_setting("nu", 0.1)
     lat.set_setting("aX_mean", 1e-5)
     sp = SimplePart()
     sp.grid_min = grid_min
+    sp.container = container
     rng = np.random.default_rng(1)
     for _ in range(count):
         sp.add(rng.uniform(-2, n + 2, 3), rng.uniform(1, 2.5), v=rng.uniform(-0.01, 0.01, 3),
@@ -92,6 +93,74 @@ def test_solid_grid_matches_linear_scan():
     fb, Fb, Tb = _many("cpu", 1)
     assert torch.equal(fa, fb)
     assert np.allclose(Fa, Fb, rtol=1e-12, atol=1e-15) and np.allclose(Ta, Tb, rtol=1e-12, atol=1e-15)
+
+
+def test_solid_tree_matches_linear_scan():
+    """bounding-volume tree container (reference SolidTree, tests/solid/main.cpp compares
+    the All/Tree/Grid indexers) gives the coupling of the full scan; only the order in
+    which a node visits its particles differs (Morton order), so the match is to rounding"""
+    fa, Fa, Ta = _many("cpu", 10 ** 9, container="all")
+    fb, Fb, Tb = _many("cpu", 10 ** 9, container="tree")
+    assert torch.allclose(fa, fb, rtol=0, atol=1e-14)
+    assert np.allclose(Fa, Fb, rtol=1e-12, atol=1e-15) and np.allclose(Ta, Tb, rtol=1e-12, atol=1e-15)
+
+
+def _tree_candidates(g, p):
+    """the kernel's stackless walk (emitter for_particle_candidates, kind 1) in Python"""
+    nl = int(g[5])
+    ids = g[8:8 + nl]
+    B = g[8 + nl:].view(np.float32).reshape(-1, 6)
+    out, node = [], 0
+    p = np.float32(p)
+    while True:
+        b = B[node]
+        inside = bool(np.all(p >= b[0:3]) and np.all(p <= b[3:6]))
+        if inside and node < nl - 1:
+            node = 2 * node + 1
+            continue
+        if inside and ids[node - (nl - 1)] >= 0:
+            out.append(int(ids[node - (nl - 1)]))
+        while node > 0 and node % 2 == 0:
+            node = (node - 1) // 2
+        if node == 0:
+            return out
+        node += 1
+
+
+@pytest.mark.parametrize("count", [1, 2, 7, 33])
+def test_solid_tree_walk_finds_every_particle_in_range(count):
+    """every particle whose cut-off sphere (rad + 2) holds a node is visited exactly once
+    by the tree walk, for any particle count (padding leaves, one-leaf tree)"""
+    rng = np.random.default_rng(count)
+    lat = Lattice("auto_d3q19_part", (40, 30, 20), device=torch.device("cpu"))
+    sp = SimplePart()
+    sp.container = "tree"
+    for _ in range(count):
+        sp.add(rng.uniform([-3, 0, 0], [43, 30, 20]), rng.uniform(1.0, 3.0))
+    sp.pre_stage(lat)
+    g = sp._d["grid"].cpu().numpy()
+    assert g[4] == 1
+    for p in rng.uniform([0, 0, 0], [40, 30, 20], (300, 3)).round():
+        got = _tree_candidates(g, p)
+        assert len(got) == len(set(got))
+        d = np.linalg.norm(sp.x - p, axis=1)
+        need = set(np.nonzero(d <= sp.r + 2)[0].tolist())
+        assert need <= set(got)
+
+
+def test_solid_container_choice_is_checked(monkeypatch):
+    monkeypatch.setenv("TCLB_SOLID_CONTAINER", "kdtree")
+    with pytest.raises(ValueError):
+        SimplePart()
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not torch.cuda.is_available(), reason="no GPU")
+def test_solid_tree_gpu_matches_cpu():
+    fa, Fa, Ta = _many("cuda", 10 ** 9, container="tree")
+    fb, Fb, Tb = _many("cpu", 10 ** 9, container="all")
+    assert torch.allclose(fa, fb, atol=1e-12)
+    assert np.allclose(Fa, Fb, rtol=1e-9, atol=1e-13) and np.allclose(Ta, Tb, rtol=1e-9, atol=1e-13)
 
 
 @pytest.mark.gpu

@@ -25,11 +25,15 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from tclb_amd.lattice import Lattice  # noqa: E402
 
 
-def _time(lat, steps, warmup):
+def _time(lat, steps, warmup, glob_every=False):
     lat.iterate(warmup, glob_last=False)
     torch.cuda.synchronize()
     t = time.perf_counter()
-    lat.iterate(steps, glob_last=True)
+    if glob_every:        # globals integrated on every step (a <Log Iterations="1"> case)
+        for _ in range(steps):
+            lat.iterate(1, glob_last=True, reduce=False)
+    else:
+        lat.iterate(steps, glob_last=True)
     torch.cuda.synchronize()
     return time.perf_counter() - t
 
@@ -94,16 +98,17 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--precision", default="double")
     ap.add_argument("--size", type=int, default=0, help="override lattice size")
+    ap.add_argument("--glob-every-step", action="store_true", help="globals on every step")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     for name in a.configs.split(","):
         fn, n, desc = CONFIGS[name]
         n = a.size or n
         lat = fn(n, a.precision, dev)
-        dt = _time(lat, a.steps, a.warmup)
+        dt = _time(lat, a.steps, a.warmup, a.glob_every_step)
         nodes = n ** 3
         out = {"config": name, "desc": desc, "model": lat.model.name, "lattice": [n, n, n],
-               "precision": a.precision, "steps": a.steps, "ms_per_step": round(dt / a.steps * 1e3, 4),
+               "precision": a.precision, "glob_every_step": a.glob_every_step, "steps": a.steps, "ms_per_step": round(dt / a.steps * 1e3, 4),
                "MLUPS": round(nodes * a.steps / dt / 1e6, 1),
                "fields": lat.nf, "stages": len(lat.model.action("Iteration").stages),
                "globals_finite": bool(all(np.isfinite(v) for v in lat.globals.values())),

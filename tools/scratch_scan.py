@@ -4,7 +4,9 @@
 Reads the gfx950 code object out of each ``_build/lib/libtclb_*_hip.so`` (``.hip_fatbin``
 section, clang-offload-bundler) and prints the stage kernels whose metadata declares a
 private segment (``.private_segment_fixed_size`` > 0: spills or runtime-indexed arrays),
-with their VGPR count.  Kernels not listed keep the whole node in registers.
+with their VGPR count and the number of scratch load/store instructions in their code
+(a frame the backend reserves, e.g. an emergency register-scavenging slot, shows as bytes
+with 0 accesses and costs nothing).  Kernels not listed keep the whole node in registers.
 
     python tools/scratch_scan.py [--lib-dir DIR] [--all]
 """
@@ -42,21 +44,34 @@ def kernel_scratch(so: str, tmp: str, kernel_filter: str = "k_stage"):
     return out
 
 
+SCRATCH_OP = re.compile(r"\b(scratch_(load|store)\w*|buffer_(load|store)\w*)\b")
+
+
+def scratch_accesses(co: str, name: str) -> int:
+    """scratch load/store instructions in the disassembly of one kernel"""
+    r = subprocess.run([f"{LLVM}/llvm-objdump", "-d", f"--disassemble-symbols={name}", co],
+                       capture_output=True, text=True)
+    return len(SCRATCH_OP.findall(r.stdout))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--lib-dir", default=os.path.join(REPO, "tclb_amd", "_build", "lib"))
     ap.add_argument("--all", action="store_true", help="also list the kernels without scratch")
     a = ap.parse_args()
     libs = sorted(glob.glob(os.path.join(a.lib_dir, "libtclb_*_hip.so")))
-    nk = nscr = 0
+    nk = nscr = nacc = 0
     with tempfile.TemporaryDirectory() as tmp:
         for so in libs:
             for scr, vgpr, name in kernel_scratch(so, tmp):
                 nk += 1
+                acc = scratch_accesses(os.path.join(tmp, "co.o"), name) if scr > 0 else 0
                 if scr > 0 or a.all:
                     nscr += scr > 0
-                    print(f"{os.path.basename(so)}\t{scr} B/lane\t{vgpr} VGPR\t{name}")
-    print(f"{len(libs)} libraries, {nk} stage kernels, {nscr} with scratch", file=sys.stderr)
+                    nacc += acc > 0
+                    print(f"{os.path.basename(so)}\t{scr} B/lane\t{acc} scratch ops\t{vgpr} VGPR\t{name}")
+    print(f"{len(libs)} libraries, {nk} stage kernels, {nscr} with a private segment, "
+          f"{nacc} with scratch accesses", file=sys.stderr)
 
 
 if __name__ == "__main__":
