@@ -109,8 +109,11 @@ TCLB_FN double zonal_read(const Launch& L, int k, int zone) {
   // z0 and L are uniform); readfirstlane of its halves lets the backend keep it in SGPRs
   // where its divergence analysis cannot tell (e.g. inside the AD node)
   const unsigned long long a = (unsigned long long)(L.zonal + ((long long)k * L.nzones + z0));
-  const unsigned long long au = (unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)a) |
-                                ((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)(a >> 32)) << 32);
+  // (readfirstlane returns int: go through unsigned, or a low word >= 2^31 would be
+  // sign-extended into the high word)
+  const unsigned lo = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)a);
+  const unsigned hi = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)(a >> 32));
+  const unsigned long long au = (unsigned long long)lo | ((unsigned long long)hi << 32);
   double r;
   asm("s_load_dwordx2 %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(r) : "s"(au));
   if (zone != z0) r = L.zonal[(long long)k * L.nzones + zone];

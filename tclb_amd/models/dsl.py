@@ -148,6 +148,7 @@ class Model:
         # hand-written reverse-mode node adjoints: stage main -> (predicate, function)
         # member names in the dynamics (see set_reverse)
         self.reverse: Dict[str, tuple] = {}
+        self.color: Optional[tuple] = None     # (value, weight) C++ expressions of Color()
         self.lattices: Dict[str, str] = {}           # group -> lattice name (weights table)
         self.defines: Dict[str, str] = {}
         self.objectives: Dict[str, str] = {}        # AddObjective: name -> expression of globals
@@ -303,6 +304,12 @@ class Model:
         load sites) instead of the forward-mode dual-number passes; the reference gets
         its reverse sweep from Tapenade (tools/makeAD)"""
         self.reverse[stage_main] = (predicate, function)
+
+    def set_color(self, value: str, weight: str = "1"):
+        """the node colour of the frame renderer (reference ``Color()``: a value mapped
+        through the colour scale and a weight, 0 drawing the node green), as C++
+        expressions of the node; the default is |U| and 0 on Solid nodes"""
+        self.color = (value, weight)
 
     def add_codegen(self, fn: Callable[["Model"], str]):
         self.codegen_blocks.append(fn)

@@ -46,5 +46,6 @@ def build() -> Model:
         m.add_node_type(n, "BOUNDARY")
     m.add_node_type("BGK", "COLLISION")
     m.add_node_type("MRT", "COLLISION")
+    m.set_color("color_value_()", "getRho() < R(1) ? 0 : 1")  # reference Color(): |U|, 0 below rho 1
     m.set_dynamics("multiphase/d2q9_kuper.inc")
     return m

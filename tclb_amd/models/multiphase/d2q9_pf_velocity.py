@@ -144,5 +144,6 @@ def build(gf=False, rt=False, outflow=False, debug=False, bgk=False, cm=False, g
     m.add_node_type("MRT", "COLLISION")
     m.options = {"GF": gf, "RT": rt, "Outflow": outflow, "GuoCM": guocm, "debug": debug, "BGK": bgk, "CM": cm,
                  "autosym": autosym}
+    m.set_color("getPhaseField()")  # reference Color(): PhaseF
     m.set_dynamics("multiphase/d2q9_pf_velocity.inc")
     return m

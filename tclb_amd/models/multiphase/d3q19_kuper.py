@@ -54,5 +54,6 @@ def build() -> Model:
     m.add_node_type("MRT", "COLLISION")
     m.add_node_type("MovingWall", "BOUNDARY")
     m.add_codegen(mrt19_block)
+    m.set_color("color_value_()", "getRho() < R(1) ? 0 : 1")  # reference Color(): |U|, 0 below rho 1
     m.set_dynamics("multiphase/d3q19_kuper.inc")
     return m

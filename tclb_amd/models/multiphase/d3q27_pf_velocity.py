@@ -291,6 +291,7 @@ def build(q27: bool = False, bgk: bool = False, thermo: bool = False, planarbenc
     m.defines["hPops"] = str(Qh)
     m.add_codegen(lambda _m: codegen(Qh))
     m.add_codegen(_field_index_block)
+    m.set_color("getPhaseField()")  # reference Color(): PhaseF, 0 on Solid
     m.set_dynamics("multiphase/d3q27_pf_velocity.inc")
     return m
 

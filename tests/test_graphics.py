@@ -69,7 +69,7 @@ def test_frame_of_channel_with_obstacle(device, tmp_path):
     m = lat.model
     fl = np.full((lat.NZ, lat.NY, nx), m.node_type("MRT").value, dtype=np.uint32)
     lat.set_flags(fl)
-    lat.set_setting("nu", 0.1)
+    lat.set_setting("Viscosity", 0.1)
     lat.set_setting("GravitationX", 1e-4)
     lat.init()
     for x in range(10, 14):
@@ -97,7 +97,7 @@ def test_graphics_element_writes_frames(tmp_path):
     xml = """<?xml version="1.0"?>
 <CLBConfig version="2.0" output="out/">
   <Geometry nx="32" ny="16"><MRT><Box/></MRT></Geometry>
-  <Model><Param name="nu" value="0.1"/><Param name="GravitationX" value="1e-4"/></Model>
+  <Model><Param name="Viscosity" value="0.1"/><Param name="GravitationX" value="1e-4"/></Model>
   <Graphics Iterations="10"/>
   <Solve Iterations="30"/>
 </CLBConfig>"""
@@ -106,3 +106,34 @@ def test_graphics_element_writes_frames(tmp_path):
     frames = sorted(f for f in os.listdir(tmp_path / "out") if f.endswith(".png"))
     assert len(frames) == 3 and frames[0].endswith("_00000010.png")
     assert _png_pixels(str(tmp_path / "out" / frames[-1])).shape == (16, 32, 4)
+
+
+@pytest.mark.parametrize("name,value", [("d2q9_pf_velocity", "PhaseField"), ("wave2D", "U")])
+def test_model_color_values(name, value):
+    """model-specific Color() (reference: the phase field for pf_velocity, the wave
+    amplitude for wave2D)"""
+    lat = Lattice(name, (24, 16, 1), device=torch.device("cpu"))
+    m = lat.model
+    coll = next((n.value for n in m.node_types if n.group == "COLLISION"), 0)
+    lat.set_flags(np.full((lat.NZ, lat.NY, 24), coll, dtype=np.uint32))
+    lat.init()
+    f = lat.fields_interior().clone()
+    f += torch.rand_like(f) * 1e-3
+    lat.set_fields_interior(f)
+    lat.iterate(2)
+    lw = lat.color().numpy()
+    q = lat.quantity(value).numpy()[0, 0]
+    assert np.allclose(lw[..., 0], q, rtol=1e-5, atol=1e-7)
+
+
+def test_kuper_color_weight():
+    """d2q9_kuper: weight 0 where the density is below 1 (reference Color())"""
+    lat = Lattice("d2q9_kuper", (24, 16, 1), device=torch.device("cpu"))
+    m = lat.model
+    coll = next(n for n in m.node_types if n.group == "COLLISION")
+    lat.set_flags(np.full((lat.NZ, lat.NY, 24), coll.value, dtype=np.uint32))
+    lat.init()
+    lat.iterate(1)
+    lw = lat.color().numpy()
+    rho = lat.quantity("Rho").numpy()[0, 0]
+    assert np.array_equal(lw[..., 1] == 0, rho < 1)
