@@ -1,0 +1,34 @@
+"""The bench.py contract the driver relies on (task spec): under torch.distributed.run
+with N ranks, rank 0 prints one JSON line with the whole-job value, n_gpus = N, the
+timed step count and the metric named in BASELINE.json.  Exercised here on the CPU with
+gloo and 2 ranks (the same code path as RCCL ranks, the device aside)."""
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run(nproc, port):
+    env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="2")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
+           "--cpu", "--shape", "32,16,16", "--steps", "3", "--warmup", "1", "--gpus", str(nproc)]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    return json.loads(lines[0])
+
+
+def test_bench_two_ranks_json_line():
+    base = json.load(open(os.path.join(ROOT, "BASELINE.json")))
+    out = _run(2, 29611)
+    assert out["n_gpus"] == 2 and out["steps"] == 3 and out["warmup"] == 1
+    assert out["value"] > 0 and out["higher_is_better"] is True
+    assert out["config"]["parallelism"] == "zslab2"
+    assert out["globals_finite"] is True
+    metric = base.get("metric") or base.get("headline", {}).get("metric")
+    if metric:
+        assert out["metric"] == metric
