@@ -83,13 +83,26 @@ examples_b) step "reference examples (part b) on the GPU, 100 its" 1100 $O/examp
 globms) step "rocprof mixed-shift globals every step" 400 $O/prof_ms_globevery.log rocprofv3 --kernel-trace --stats -d $O/prof_ms_globevery -o run --output-format csv -- python3 $R/bench.py --steps 10 --warmup 2 --glob-every-step --precision mixed-shift ;;
 smoke) step "smoke" 300 $O/smoke.log python -c "import __graft_entry__ as g; g.smoke()" ;;
 bench1) step "bench fp64" 300 $O/bench_fp64.json python bench.py ;;
+r03k)
+  for r in a b; do
+    step "pf384 mixed-shift globals every step ($r)" 300 $O/pf384_ms_glob_$r.log python tools/bench_configs.py --configs pf384 --precision mixed-shift --glob-every-step
+    step "pf384 mixed-shift globals every step, gw2 ($r)" 300 $O/pf384_ms_glob_gw2_$r.log env TCLB_VARIANT=gw2 python tools/bench_configs.py --configs pf384 --precision mixed-shift --glob-every-step
+  done
+  step "pf384 fp64 globals every step, gw2" 300 $O/pf384_fp64_glob_gw2.log env TCLB_VARIANT=gw2 python tools/bench_configs.py --configs pf384 --glob-every-step
+  step "pf384 fp64 / mixed-shift plain" 300 $O/pf384_plain.log bash -c 'python tools/bench_configs.py --configs pf384 && python tools/bench_configs.py --configs pf384 --precision mixed-shift'
+  step "d3q27 mixed-shift globals every step, gw2" 300 $O/bench_ms_glob_gw2.json env TCLB_VARIANT=gw2 python bench.py --steps 50 --precision mixed-shift --glob-every-step
+  step "rocprof part256 grid" 300 $O/prof_part256.log rocprofv3 --kernel-trace --stats -d $O/prof_part256 -o run --output-format csv -- python3 $R/tools/bench_configs.py --configs part256 --steps 20 --warmup 3
+  step "rocprof part256 tree" 300 $O/prof_part256_tree.log env TCLB_SOLID_CONTAINER=tree rocprofv3 --kernel-trace --stats -d $O/prof_part256_tree -o run --output-format csv -- python3 $R/tools/bench_configs.py --configs part256 --steps 20 --warmup 3
+  step "adjoint tests" 600 $O/pytest_gpu_adjoint.log python -u -m pytest tests/test_gpu_adjoint.py tests/test_adjoint_reverse.py tests/test_adjoint_dist.py -v -m gpu --timeout 300 --timeout-method thread
+  step "adjoint bench 128" 400 $O/bench_adjoint_128.json python tools/bench_adjoint.py --size 128 --steps 80 ;;
+pfprof)
+  step "rocprof pf384 mixed-shift" 400 $O/prof_pf384_ms.log rocprofv3 --kernel-trace --stats -d $O/prof_pf384_ms -o run --output-format csv -- python3 $R/tools/bench_configs.py --configs pf384 --precision mixed-shift --steps 5 --warmup 1
+  step "counters pf384 mixed-shift" 500 $O/counters_pf384_ms.log python tools/counters.py --tag pf384_mixed_shift --nodes 56623104 --outdir $O/counters -- python3 $R/tools/bench_configs.py --configs pf384 --steps 5 --warmup 1 --precision mixed-shift ;;
 r03i)
   step "part256 grid container" 300 $O/part256_grid.log python tools/bench_configs.py --configs part256
   step "part256 tree container" 300 $O/part256_tree.log env TCLB_SOLID_CONTAINER=tree python tools/bench_configs.py --configs part256
-  step "pf384 mixed-shift, scalar zonal reads" 300 $O/pf384_ms_a.log python tools/bench_configs.py --configs pf384 --precision mixed-shift
-  step "pf384 mixed-shift, vector zonal reads" 300 $O/pf384_ms_zvec_a.log env TCLB_VARIANT=zvec python tools/bench_configs.py --configs pf384 --precision mixed-shift
-  step "pf384 mixed-shift, scalar zonal reads (2)" 300 $O/pf384_ms_b.log python tools/bench_configs.py --configs pf384 --precision mixed-shift
-  step "pf384 mixed-shift, vector zonal reads (2)" 300 $O/pf384_ms_zvec_b.log env TCLB_VARIANT=zvec python tools/bench_configs.py --configs pf384 --precision mixed-shift
+  step "pf384 mixed-shift, scalar zonal reads" 300 $O/pf384_ms_zscal_a.log env TCLB_VARIANT=zscal python tools/bench_configs.py --configs pf384 --precision mixed-shift
+  step "pf384 mixed-shift, vector zonal reads" 300 $O/pf384_ms_a.log python tools/bench_configs.py --configs pf384 --precision mixed-shift
   step "pf384 fp64 + globals every step" 300 $O/pf384_fp64_glob.log bash -c 'python tools/bench_configs.py --configs pf384 && python tools/bench_configs.py --configs pf384 --glob-every-step'
   step "pf384 mixed-shift globals every step" 300 $O/pf384_ms_glob.log python tools/bench_configs.py --configs pf384 --precision mixed-shift --glob-every-step
   step "d3q27 bench fp64 / globals every step" 400 $O/bench_glob.log bash -c 'python bench.py --steps 50 && python bench.py --steps 50 --glob-every-step && python bench.py --steps 50 --precision mixed-shift && python bench.py --steps 50 --precision mixed-shift --glob-every-step' ;;

@@ -299,8 +299,11 @@ class Adjoint:
             lat.snaps[lat.cur].copy_(snaps[base])
             lat.iter = it0 + base
             states = [snaps[base]]
+            # a single rank reads no ghost plane, and a step that writes every field
+            # overwrites the whole interior: the recompute buffers need no zero fill
+            uninit = not lat.ghosts and lat.writes_all_fields(action)
             for t in range(base + 1, end if keep_segment else base + 1):
-                lat.snaps[1 - lat.cur] = lat.new_snapshot()
+                lat.snaps[1 - lat.cur] = lat.new_snapshot(uninit)
                 lat.iterate(1, glob_last=False, action=action)
                 states.append(lat.snaps[lat.cur])
             for t in range(end - 1, base - 1, -1):

@@ -39,8 +39,10 @@ VARIANTS = {
     # occupancy floor for the fp32/fp16-storage kernels (executor_hip.hpp k_stage_narrow)
     "nw3": ["-DTCLB_NT_STORE=1", "-DTCLB_NARROW_WAVES=3"],
     "nw4": ["-DTCLB_NT_STORE=1", "-DTCLB_NARROW_WAVES=4"],
-    # zonal settings read with plain per-lane vector loads (core.hpp zonal_read A/B)
-    "zvec": ["-DTCLB_NT_STORE=1", "-DTCLB_ZONAL_SCALAR=0"],
+    # zonal settings read by scalar loads for the wave's first zone (core.hpp zonal_read A/B)
+    "zscal": ["-DTCLB_NT_STORE=1", "-DTCLB_ZONAL_SCALAR=1"],
+    # globals-integrating stage kernels held to 2 waves/SIMD (executor_hip.hpp k_stage_glob)
+    "gw2": ["-DTCLB_NT_STORE=1", "-DTCLB_GLOB_WAVES=2"],
 }
 DEFAULT_VARIANT = os.environ.get("TCLB_VARIANT", "")
 # CPU executor variants: "ubsan" builds the node code with UndefinedBehaviorSanitizer

@@ -97,10 +97,11 @@ struct Launch {
 // collision).  On the GPU the value of the zone of the wave's first lane is fetched by a
 // scalar load (s_load: constant cache, short latency; a read, the table is never written
 // by a kernel); only lanes of another zone issue the vector load, and a wave with a single
-// zone (nearly all of them) skips it.  -DTCLB_ZONAL_SCALAR=0 (build variant "zvec") keeps
-// the plain load for A/B runs.
+// zone (nearly all of them) skips it.  Build variant "zscal" (-DTCLB_ZONAL_SCALAR=1); the
+// default keeps the plain load: on pf384 mixed-shift the scalar reads measured 1 % slower
+// (profiles/README.md r03j), the zonal loads are not what limits that kernel.
 #ifndef TCLB_ZONAL_SCALAR
-#define TCLB_ZONAL_SCALAR 1
+#define TCLB_ZONAL_SCALAR 0
 #endif
 TCLB_FN double zonal_read(const Launch& L, int k, int zone) {
 #if TCLB_GPU && defined(__HIP_DEVICE_COMPILE__) && TCLB_ZONAL_SCALAR

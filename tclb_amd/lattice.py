@@ -169,11 +169,23 @@ class Lattice:
         self.particles = None     # ParticleSystem with pre_stage/post_stage/step hooks
         self.average_start = 0
 
-    def new_snapshot(self) -> torch.Tensor:
+    def new_snapshot(self, uninit: bool = False) -> torch.Tensor:
         """a zeroed snapshot buffer with the layout of snaps[0/1] ([nf][NZ][NY][px], field
-        stride fs): the A/B pair, and states kept by the adjoint's checkpointing"""
-        return (torch.zeros(self.nf * self.fs, dtype=self.sdtype, device=self.device)
+        stride fs): the A/B pair, and states kept by the adjoint's checkpointing.
+        uninit: no zero fill, for a buffer the next step overwrites in full (every field
+        of every interior node); padding columns and ghost planes are then undefined"""
+        alloc = torch.empty if uninit else torch.zeros
+        return (alloc(self.nf * self.fs, dtype=self.sdtype, device=self.device)
                 .as_strided((self.nf, self.NZ, self.NY, self.px), (self.fs, self.NY * self.px, self.px, 1)))
+
+    def writes_all_fields(self, action: str = "Iteration") -> bool:
+        """every field is saved by some stage of `action` (its output snapshot holds no
+        value from before the step)"""
+        m = self.model
+        saved = set()
+        for sname in m.action(action).stages:
+            saved.update(self._saved_fields(m.stage(sname)))
+        return len(saved) == self.nf
 
     # ------------------------------------------------------------------ launch
     def _base_launch(self) -> abi.Launch:

@@ -1,8 +1,8 @@
 """Hand-written reverse sweeps of the node update (Model.set_reverse; d3q19_adj rev_run,
 the counterpart of the reference's Tapenade Run_b) against the dual-number adjoint of the
 same node code: the unsteady adjoint state, the objective and the design gradient agree
-to rounding, with boundary nodes (Zou/He planes: dual passes) and MRT nodes (reverse
-sweep) in one lattice, objectives on Inlet/Outlet planes and the material penalty; with a
+to rounding, with Zou/He pressure and velocity planes, bounce-back, solid, flag-free and
+non-MRT nodes (reverse sweeps) and a limited-pressure node (dual passes) in one lattice, objectives on Inlet/Outlet planes and the material penalty; with a
 seeded setting the sweeps step aside (dual passes everywhere)."""
 import numpy as np
 import pytest
@@ -24,10 +24,15 @@ def _case(device, reverse, settings=()):
     fl[:, :, 2] |= m.node_type("Inlet").value
     fl[:, :, 4:7] |= m.node_type("DesignSpace").value
     fl[:, 0, 3] = m.node_type("Wall").value
+    fl[:, 1, 9] = m.node_type("WVelocity").value | mrt
+    fl[:, 2, 9] = m.node_type("Solid").value | mrt
+    fl[:, 3, 9] = m.node_type("WPressureL").value | mrt
+    fl[:, 4, 9] = m.node_type("BGK").value
+    fl[2, 5, 10] = 0
     lat.set_flags(fl)
     for k, v in {"nu": 0.1, "InletDensity": 1.03, "FluxInObj": 1.0, "EnergyFluxInObj": 0.3,
                  "PressureFluxInObj": -0.2, "PressureDiffInObj": 0.7, "MaterialPenaltyInObj": 0.05,
-                 "Theta": 1.3}.items():
+                 "Theta": 1.3, "InletVelocity": 0.01}.items():
         lat.set_setting(k, v)
     lat.init()
     wi = m.field_index("w")
