@@ -95,6 +95,14 @@ r03k)
   step "rocprof part256 tree" 300 $O/prof_part256_tree.log env TCLB_SOLID_CONTAINER=tree rocprofv3 --kernel-trace --stats -d $O/prof_part256_tree -o run --output-format csv -- python3 $R/tools/bench_configs.py --configs part256 --steps 20 --warmup 3
   step "adjoint tests" 600 $O/pytest_gpu_adjoint.log python -u -m pytest tests/test_gpu_adjoint.py tests/test_adjoint_reverse.py tests/test_adjoint_dist.py -v -m gpu --timeout 300 --timeout-method thread
   step "adjoint bench 128" 400 $O/bench_adjoint_128.json python tools/bench_adjoint.py --size 128 --steps 80 ;;
+r03l)
+  step "configs fp64 (cavity, pf384, part256)" 600 $O/configs_fp64.log python tools/bench_configs.py
+  step "part256 tree container" 300 $O/part256_tree.log env TCLB_SOLID_CONTAINER=tree python tools/bench_configs.py --configs part256
+  step "pf384 globals every step (fp64, mixed-shift)" 400 $O/pf384_glob.log bash -c 'python tools/bench_configs.py --configs pf384 --glob-every-step && python tools/bench_configs.py --configs pf384 --precision mixed-shift --glob-every-step && python tools/bench_configs.py --configs pf384 --precision mixed-shift'
+  step "heavy models globals every step, default vs gw2 cap" 600 $O/heavy_glob_ab.log python tools/perf_models.py --models d3q27_pf_velocity_thermo,d3q27_pf_velocity_OutFlow,d3q27_tePSM_per_NEBB --n3 192 --steps 6 --glob-every-step --variants ",gw2"
+  step "heavy models plain steps" 400 $O/heavy_plain.log python tools/perf_models.py --models d3q27_pf_velocity_thermo,d3q27_pf_velocity_OutFlow,d3q27_tePSM_per_NEBB --n3 192 --steps 6
+  step "adjoint bench 128" 400 $O/bench_adjoint_128.json python tools/bench_adjoint.py --size 128 --steps 80
+  step "bench fp64" 300 $O/bench_fp64.json python bench.py ;;
 pfprof)
   step "rocprof pf384 mixed-shift" 400 $O/prof_pf384_ms.log rocprofv3 --kernel-trace --stats -d $O/prof_pf384_ms -o run --output-format csv -- python3 $R/tools/bench_configs.py --configs pf384 --precision mixed-shift --steps 5 --warmup 1
   step "counters pf384 mixed-shift" 500 $O/counters_pf384_ms.log python tools/counters.py --tag pf384_mixed_shift --nodes 56623104 --outdir $O/counters -- python3 $R/tools/bench_configs.py --configs pf384 --steps 5 --warmup 1 --precision mixed-shift ;;

@@ -41,8 +41,10 @@ VARIANTS = {
     "nw4": ["-DTCLB_NT_STORE=1", "-DTCLB_NARROW_WAVES=4"],
     # zonal settings read by scalar loads for the wave's first zone (core.hpp zonal_read A/B)
     "zscal": ["-DTCLB_NT_STORE=1", "-DTCLB_ZONAL_SCALAR=1"],
-    # globals-integrating stage kernels held to 2 waves/SIMD (executor_hip.hpp k_stage_glob)
+    # globals-integrating stage kernels: 2 waves/SIMD for every model / no cap for any
+    # (executor_hip.hpp k_stage_glob; the default follows Model.glob_waves)
     "gw2": ["-DTCLB_NT_STORE=1", "-DTCLB_GLOB_WAVES=2"],
+    "gw0": ["-DTCLB_NT_STORE=1", "-DTCLB_GLOB_WAVES=0"],
 }
 DEFAULT_VARIANT = os.environ.get("TCLB_VARIANT", "")
 # CPU executor variants: "ubsan" builds the node code with UndefinedBehaviorSanitizer
@@ -374,6 +376,46 @@ def bench_lib_path(name: str) -> str:
     return os.path.join(LIB, f"libtclb_{name}.so")
 
 
+def build_device_runtime(force: bool = False, verbose: bool = False) -> Optional[str]:
+    """model-independent HIP kernels of the runtime (csrc/device/*.hip: the per-step
+    particle kernels) -> _build/lib/libtclb_device.so"""
+    if not os.path.exists(HIPCC):
+        return None
+    ddir = os.path.join(CSRC, "device")
+    srcs = sorted(os.path.join(ddir, f) for f in os.listdir(ddir) if f.endswith(".hip"))
+    target = os.path.join(LIB, "libtclb_device.so")
+    os.makedirs(LIB, exist_ok=True)
+    cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", *srcs, "-o"]
+    h = _hash_inputs(srcs, " ".join(cmd))
+    stamp = target + ".hash"
+    if not force and os.path.exists(target) and os.path.exists(stamp) and open(stamp).read() == h:
+        return target
+    tmp = f"{target}.{os.getpid()}.tmp"
+    r = subprocess.run(cmd + [tmp], capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"device runtime build failed:\n{r.stderr[-10000:]}")
+    os.replace(tmp, target)
+    with open(stamp, "w") as f:
+        f.write(h)
+    if verbose:
+        print("[tclb build] device runtime", flush=True)
+    return target
+
+
+def device_runtime_stale() -> Optional[str]:
+    """why libtclb_device.so cannot be used as is (None: fresh)"""
+    ddir = os.path.join(CSRC, "device")
+    srcs = sorted(os.path.join(ddir, f) for f in os.listdir(ddir) if f.endswith(".hip"))
+    target = os.path.join(LIB, "libtclb_device.so")
+    cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", *srcs, "-o"]
+    if not os.path.exists(target):
+        return "missing"
+    stamp = target + ".hash"
+    if not os.path.exists(stamp) or open(stamp).read() != _hash_inputs(srcs, " ".join(cmd)):
+        return "sources changed"
+    return None
+
+
 def build_bench_libs(force: bool = False, verbose: bool = False) -> Dict[str, str]:
     """stand-alone HIP micro-benchmarks (csrc/bench/<name>.hip -> _build/lib/libtclb_<name>.so),
     e.g. the LDS A/B of the 27-point stencil (tools/lds_ab.py)"""
@@ -409,6 +451,7 @@ def build_all(models: Optional[List[str]] = None, kinds=("cpu", "hip"), jobs: in
               verbose=False) -> Dict[str, Dict[str, str]]:
     models = models or registry.names()
     build_host(force=force, verbose=verbose)
+    build_device_runtime(force=force, verbose=verbose)
     build_tools(force=force, verbose=verbose)
     jobs = jobs or max(1, min(8, os.cpu_count() or 1))
     tasks = [(m, k) for m in models for k in kinds]

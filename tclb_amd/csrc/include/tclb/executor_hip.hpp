@@ -126,17 +126,22 @@ k_stage_narrow(const Launch L) {
 }
 #endif
 
-// Occupancy floor of the globals-integrating instantiations (build variant, e.g.
-// -DTCLB_GLOB_WAVES=2): the GLOB=true kernel keeps the globals accumulators live through
-// the whole node, which can push it past 256 VGPRs into 1 wave/SIMD (pf_velocity
-// mixed-shift: 266 VGPRs, 2.3x the plain step); amdgpu_waves_per_eu caps it.
-#ifdef TCLB_GLOB_WAVES
-template <class Model, class R, class S, int STG>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TCLB_GLOB_WAVES)))
-k_stage_glob(const Launch L) {
+// Occupancy floor of the globals-integrating instantiations: the GLOB=true kernel keeps
+// the globals accumulators live through the whole node, which can push it past 256 VGPRs
+// into 1 wave/SIMD (pf_velocity mixed-shift: 266 VGPRs, 2.3x the plain step;
+// profiles/README.md r03j/r03k).  amdgpu_waves_per_eu(W) caps it, W = the model's
+// GLOB_WAVES_ (DSL Model.glob_waves; 0 = no cap, for kernels far above 256 VGPRs where a
+// cap would spill heavily); -DTCLB_GLOB_WAVES=W overrides it for A/B builds.
+#ifndef TCLB_GLOB_WAVES
+#define TCLB_GLOB_WAVES -1
+#endif
+template <class Model>
+constexpr int glob_waves() { return TCLB_GLOB_WAVES >= 0 ? TCLB_GLOB_WAVES : Model::GLOB_WAVES_; }
+
+template <class Model, class R, class S, int STG, int W>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W))) k_stage_glob(const Launch L) {
   stage_body<Model, R, S, STG, true>(L);
 }
-#endif
 
 template <class Model, class R, class S>
 __global__ void __launch_bounds__(256) k_quantity(const Launch L) {
@@ -185,12 +190,10 @@ inline void launch_shape(const Launch& L, dim3& grid, dim3& block, int sbytes = 
 
 template <class Model, class R, class S, int I, bool G>
 inline bool launch_one(const Launch& L, dim3 grid, dim3 block, hipStream_t s) {
-#ifdef TCLB_GLOB_WAVES
-  if constexpr (G) {
-    k_stage_glob<Model, R, S, I><<<grid, block, 0, s>>>(L);
+  if constexpr (G && glob_waves<Model>() > 0) {
+    k_stage_glob<Model, R, S, I, glob_waves<Model>()><<<grid, block, 0, s>>>(L);
     return true;
   }
-#endif
 #ifdef TCLB_NARROW_WAVES
   if constexpr (sizeof(S) < sizeof(double)) {
     k_stage_narrow<Model, R, S, I, G><<<grid, block, 0, s>>>(L);

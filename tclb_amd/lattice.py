@@ -485,7 +485,13 @@ class Lattice:
 
     # ------------------------------------------------------------------ actions
     def _saved_fields(self, stage) -> List[int]:
-        return [i for i, f in enumerate(self.model.fields) if self.model.matches(f, stage.save_fields)]
+        # cached per stage: the per-step paths (halo, particles, adjoint) ask every launch
+        cache = self.__dict__.setdefault("_saved_cache", {})
+        key = (stage.name, tuple(stage.save_fields) if stage.save_fields is not None else None)
+        r = cache.get(key)
+        if r is None:
+            r = cache[key] = [i for i, f in enumerate(self.model.fields) if self.model.matches(f, stage.save_fields)]
+        return r
 
     def run_action(self, name: str, glob: bool = False, reduce: bool = True):
         """one action; with glob the globals are integrated and (reduce) all-reduced and

@@ -149,6 +149,9 @@ class Model:
         # member names in the dynamics (see set_reverse)
         self.reverse: Dict[str, tuple] = {}
         self.color: Optional[tuple] = None     # (value, weight) C++ expressions of Color()
+        # waves/SIMD floor of the globals-integrating stage kernels (0: compiler's choice);
+        # see executor_hip.hpp k_stage_glob
+        self.glob_waves: int = 2
         self.lattices: Dict[str, str] = {}           # group -> lattice name (weights table)
         self.defines: Dict[str, str] = {}
         self.objectives: Dict[str, str] = {}        # AddObjective: name -> expression of globals

@@ -95,4 +95,5 @@ def build(nebb: bool = False, sup: bool = False, isothermal: bool = False) -> Mo
     if not isothermal:
         m.add_codegen(lambda _m: f"  static constexpr int FI_H0 = {_m.field_index('h[0]')};")
     m.set_dynamics("heat/d3q27_tepsm_per.inc")
+    m.glob_waves = 0          # 410-440 VGPRs: a 2-wave cap would spill heavily
     return m

@@ -157,4 +157,5 @@ def build(outflowconvective=False, outflowneumann=False, avg=False, ibb=False, s
                  "IBB": ibb, "SMAG": smag, "CHT": cht}
     m.add_codegen(_blocks)
     m.set_dynamics(f"heat/{name}.inc")
+    m.glob_waves = 0 if outflowconvective else 2     # OutFlowConvective: 316-394 VGPRs
     return m

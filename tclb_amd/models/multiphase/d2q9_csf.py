@@ -137,4 +137,5 @@ def build(bc=False, bcinit=False, noflow=False, weno=False, viscstep=False, cumu
         return "\n".join(out)
     m.add_codegen(blocks)
     m.set_dynamics("multiphase/d2q9_csf.inc")
+    m.glob_waves = 0 if weno else 2                  # WENO/cumulant: 326-334 VGPRs
     return m

@@ -293,6 +293,9 @@ def build(q27: bool = False, bgk: bool = False, thermo: bool = False, planarbenc
     m.add_codegen(_field_index_block)
     m.set_color("getPhaseField()")  # reference Color(): PhaseF, 0 on Solid
     m.set_dynamics("multiphase/d3q27_pf_velocity.inc")
+    # GLOB kernels of the thermo / OutFlow variants need 310-370 VGPRs: a 2-wave cap would
+    # spill a quarter of them; the plain pf_velocity (250-266) gains 1.5x from it
+    m.glob_waves = 0 if (thermo or outflow) else 2
     return m
 
 

@@ -225,8 +225,12 @@ class ParticleSystem:
         if lat.comm.distributed and lat.comm.size > 1:
             acc.copy_(lat.comm.allreduce_globals(acc.reshape(-1).clone(), acc.numel()).reshape(acc.shape))
         # a NaN force is dropped (reference Lattice.cu.Rt:420-435 zeroes it with a notice;
-        # the check stays on the device, no host round trip)
-        acc.masked_fill_(torch.isnan(acc), 0.0)
+        # the check stays on the device, no host round trip): one HIP kernel on a GPU
+        if acc.is_cuda:
+            from ..ops import device as D
+            D.nan_to_zero(acc, lat._stream())
+        else:
+            acc.masked_fill_(torch.isnan(acc), 0.0)
         self._host_stale |= {"force", "torque"}
         self.detach(lat)
 
@@ -271,11 +275,19 @@ class SimplePart(ParticleSystem):
         self.logged: List[int] = []
         self.iteration = 0
 
-    def _integrate(self):
+    def _integrate(self, lat=None):
         """the update of integrate_rigid, vectorised over the particles on the device:
-        v += F/m + a; x += v; omega += T/I (I = 2/5 m r^2); periodic wrap"""
+        v += F/m + a; x += v; omega += T/I (I = 2/5 m r^2); periodic wrap.  On a GPU one
+        HIP kernel (csrc/device/particles.hip), else tensor ops"""
         d, n = self._d, self.n
         if n == 0:
+            return
+        if d["P"].is_cuda:
+            from ..ops import device as D
+            bits = sum(1 << k for k in range(3) if self.periodic[k])
+            stream = lat._stream() if lat is not None else torch.cuda.current_stream(d["P"].device).cuda_stream
+            D.rigid_step(d["P"], d["acc"], d["m"], d["free"], n, self.acc, bits, self.period, stream)
+            self._host_stale |= {"x", "v", "omega"}
             return
         P, acc = d["P"][:n], d["acc"][:n]
         x, v, w, r = P[:, 0:3], P[:, 3:6], P[:, 6:9], P[:, 9]
@@ -295,7 +307,7 @@ class SimplePart(ParticleSystem):
 
     def step(self, lat):
         self.iteration += 1
-        self._integrate()
+        self._integrate(lat)
         if self.log_path and self.iteration % self.log_every == 0 and lat.comm.rank == 0:
             self._log()
 

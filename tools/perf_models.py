@@ -23,6 +23,7 @@ def main():
     ap.add_argument("--precision", default="double")
     ap.add_argument("--variants", default="", help="comma list of HIP build variants to A/B (interleaved)")
     ap.add_argument("--rounds", type=int, default=1)
+    ap.add_argument("--glob-every-step", action="store_true", help="globals integrated on every step")
     a = ap.parse_args()
     variants = a.variants.split(",") if a.variants else [None]
     names = a.models.split(",") if a.models else registry.names()
@@ -38,13 +39,17 @@ def main():
             lat.iterate(3, glob_last=False)
             torch.cuda.synchronize()
             t = time.perf_counter()
-            lat.iterate(a.steps, glob_last=False)
+            if a.glob_every_step:
+                for _ in range(a.steps):
+                    lat.iterate(1, glob_last=True, reduce=False)
+            else:
+                lat.iterate(a.steps, glob_last=False)
             torch.cuda.synchronize()
             dt = (time.perf_counter() - t) / a.steps
             es = lat.snaps[0].element_size()
             nodes = shape[0] * shape[1] * shape[2]
             bpn = 2 * lat.nf * es + lat.flags.element_size()
-            print(json.dumps({"model": name, "variant": variant, "round": rnd, "shape": shape, "fields": lat.nf, "stages": len(m.stages),
+            print(json.dumps({"model": name, "variant": variant, "round": rnd, "glob_every_step": a.glob_every_step, "shape": shape, "fields": lat.nf, "stages": len(m.stages),
                               "ms": round(dt * 1e3, 3), "MLUPS": round(nodes / dt / 1e6, 1),
                               "GBps_meter": round(nodes * bpn / dt / 1e9, 1)}), flush=True)
             del lat
