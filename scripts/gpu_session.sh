@@ -103,6 +103,18 @@ r03l)
   step "heavy models plain steps" 400 $O/heavy_plain.log python tools/perf_models.py --models d3q27_pf_velocity_thermo,d3q27_pf_velocity_OutFlow,d3q27_tePSM_per_NEBB --n3 192 --steps 6
   step "adjoint bench 128" 400 $O/bench_adjoint_128.json python tools/bench_adjoint.py --size 128 --steps 80
   step "bench fp64" 300 $O/bench_fp64.json python bench.py ;;
+r03n)
+  step "configs fp64 (cavity, pf384, part256)" 600 $O/configs_fp64.log python tools/bench_configs.py
+  step "configs mixed-shift (pf384)" 300 $O/configs_ms.log python tools/bench_configs.py --configs pf384 --precision mixed-shift
+  step "part256 host time per step (32^3)" 300 $O/part32_host.log python tools/bench_configs.py --configs part256 --size 32 --steps 300 --warmup 20
+  step "rocprof part256 trace" 300 $O/prof_part256.log rocprofv3 --kernel-trace --stats -d $O/prof_part256 -o run --output-format csv -- python3 $R/tools/bench_configs.py --configs part256 --steps 20 --warmup 3
+  step "counters pf384 mixed-shift (waves, instruction mix)" 500 $O/counters_pf384_ms.log python tools/counters.py --tag pf384_ms_mix --passes 2,3 --nodes 56623104 --outdir $O/counters -- python3 $R/tools/bench_configs.py --configs pf384 --steps 3 --warmup 1 --precision mixed-shift
+  step "counters pf384 fp64 (waves, instruction mix)" 500 $O/counters_pf384.log python tools/counters.py --tag pf384_fp64_mix --passes 2,3 --nodes 56623104 --outdir $O/counters -- python3 $R/tools/bench_configs.py --configs pf384 --steps 3 --warmup 1 ;;
+r03o)
+  for v in "" gregs flataddr; do
+    step "d3q27 fp64/ms +- globals every step, variant '$v'" 400 $O/bench_glob_${v:-default}.log bash -c "TCLB_VARIANT=$v python bench.py --steps 50 && TCLB_VARIANT=$v python bench.py --steps 50 --glob-every-step && TCLB_VARIANT=$v python bench.py --steps 50 --precision mixed-shift && TCLB_VARIANT=$v python bench.py --steps 50 --precision mixed-shift --glob-every-step"
+    step "pf384 fp64/ms +- globals every step, variant '$v'" 500 $O/pf384_${v:-default}.log bash -c "export TCLB_VARIANT=$v; python tools/bench_configs.py --configs pf384,cavity,part256 && python tools/bench_configs.py --configs pf384 --glob-every-step && python tools/bench_configs.py --configs pf384,cavity --precision mixed-shift && python tools/bench_configs.py --configs pf384 --precision mixed-shift --glob-every-step"
+  done ;;
 pfprof)
   step "rocprof pf384 mixed-shift" 400 $O/prof_pf384_ms.log rocprofv3 --kernel-trace --stats -d $O/prof_pf384_ms -o run --output-format csv -- python3 $R/tools/bench_configs.py --configs pf384 --precision mixed-shift --steps 5 --warmup 1
   step "counters pf384 mixed-shift" 500 $O/counters_pf384_ms.log python tools/counters.py --tag pf384_mixed_shift --nodes 56623104 --outdir $O/counters -- python3 $R/tools/bench_configs.py --configs pf384 --steps 5 --warmup 1 --precision mixed-shift ;;

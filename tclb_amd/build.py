@@ -45,6 +45,11 @@ VARIANTS = {
     # (executor_hip.hpp k_stage_glob; the default follows Model.glob_waves)
     "gw2": ["-DTCLB_NT_STORE=1", "-DTCLB_GLOB_WAVES=2"],
     "gw0": ["-DTCLB_NT_STORE=1", "-DTCLB_GLOB_WAVES=0"],
+    # A/B of the round-3 defaults: per-thread register globals accumulators reduced at the
+    # end of the block (executor_hip.hpp TCLB_GLOB_LDS=0); one 64-bit flat address per
+    # access instead of SGPR row base + 32-bit lane offset (core.hpp TCLB_ROW_ADDR=0)
+    "gregs": ["-DTCLB_NT_STORE=1", "-DTCLB_GLOB_LDS=0"],
+    "flataddr": ["-DTCLB_NT_STORE=1", "-DTCLB_ROW_ADDR=0"],
 }
 DEFAULT_VARIANT = os.environ.get("TCLB_VARIANT", "")
 # CPU executor variants: "ubsan" builds the node code with UndefinedBehaviorSanitizer
@@ -134,6 +139,9 @@ def _cmd(kind: str, src: str, out: str, gen_dir: str, variant: str = "") -> List
         # of scratch in the d3q27_cumulant fp64 kernel).
         return [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
                 "-munsafe-fp-atomics", "-mllvm", "-simplifycfg-sink-common=false",
+                # AddTo<global> into LDS (core.hpp glob_add): a DPP wave reduction + one
+                # LDS atomic per wave instead of the default lane-by-lane loop
+                "-mllvm", "-amdgpu-atomic-optimizer-strategy=DPP",
                 "-Wno-unused-result", "-Wno-pass-failed", *VARIANTS[variant], *incs,
                 src, "-o", out]
     opt = "-O2" if kind == "ad" else "-O3"

@@ -8,6 +8,7 @@
 #include <stdint.h>
 #include <math.h>
 #include <stddef.h>
+#include <type_traits>
 
 #if defined(__HIPCC__)
 #include <hip/hip_runtime.h>
@@ -204,18 +205,43 @@ struct Addr {
     sy = (int)L.sy; sz = (int)L.sz;
     node = x + sy * (y + gy) + sz * (z + gz);
   }
-  TCLB_FN int off(int dx, int dy, int dz) const {
+  // x part (lane-varying on the GPU: a wave is 64 consecutive x of one row) and y/z part
+  // (wave-uniform there: the executors pass y and z through readfirstlane) of off()
+  TCLB_FN int xo(int dx) const {
 #ifdef TCLB_DEBUG_NO_XSHIFT
     dx = 0;  // diagnostic build only: aligned-x ceiling of the access pattern (wrong physics)
 #endif
-    int xx = dx == 0 ? x : wrap(x + dx, nx);
+    return dx == 0 ? x : wrap(x + dx, nx);
+  }
+  TCLB_FN int yzo(int dy, int dz) const {
     int yy = y + dy;
     if (dy != 0 && gy == 0) yy = wrap(yy, ny);
     int zz = z + dz;
     if (dz != 0 && gz == 0) zz = wrap(zz, nz);
-    return xx + sy * (yy + gy) + sz * (zz + gz);
+    return sy * (yy + gy) + sz * (zz + gz);
   }
+  TCLB_FN int off(int dx, int dy, int dz) const { return xo(dx) + yzo(dy, dz); }
 };
+
+// Element x of a row whose (uniform) start is `row`: on the GPU the row pointer lives in
+// SGPRs and the lane's x goes in as a 32-bit zero-extended byte offset, so every access is
+// one global_load/store with SGPR base + VGPR offset (saddr form) and the few distinct x
+// offsets of a stencil (x-1, x, x+1) are shared by all fields; with the whole offset in a
+// sign-extended int each access needed its own 64-bit VGPR address (two VGPRs and a
+// v_lshl_add_u64 per load; 84 of them in the pf_velocity collide).  x < 2^28: a row is
+// shorter than a field.
+#ifndef TCLB_ROW_ADDR
+#define TCLB_ROW_ADDR 1
+#endif
+template <class T>
+TCLB_FN T* row_at(T* row, int x) {
+#if TCLB_GPU && defined(__HIP_DEVICE_COMPILE__) && TCLB_ROW_ADDR
+  typedef typename std::conditional<std::is_const<T>::value, const char, char>::type C;
+  return (T*)((C*)row + (unsigned)(x * (int)sizeof(T)));
+#else
+  return row + x;
+#endif
+}
 
 // Streaming loads/stores.  Every population is read once and written once per step,
 // so non-temporal hints keep the 4 MB/XCD L2 for the x-misaligned neighbour lines.
@@ -435,6 +461,39 @@ inline int prec_dispatch(int prec, F&& f) {
   }                                                                                           \
   extern "C" int tclb_##NAME##_sizeof_sample_plan() { return (int)sizeof(tclb::SamplePlan); } \
   extern "C" int tclb_##NAME##_sizeof_launch() { return (int)sizeof(tclb::Launch); }
+
+// Globals accumulation of one node (the emitted AddTo<global>).  `g` is the executor's
+// accumulator array: per-thread registers on the CPU and in the AD executors; on the GPU
+// primal executor a block-shared LDS array (executor_hip.hpp stage_body), so the GLOB
+// instantiation keeps no NG-long accumulator live through the node (pf_velocity: 33
+// globals = 66 VGPRs, 266 VGPRs in all, 1 wave/SIMD; profiles/README.md r03j).  The LDS
+// add is a wave reduction (DPP, -amdgpu-atomic-optimizer-strategy=DPP: correct under
+// divergence) and one ds_add/ds_max per wave.  __builtin_amdgcn_is_shared folds at
+// compile time once the accumulator's address space is known.
+template <class R>
+TCLB_FN void glob_add(R* g, int i, R v) {
+#if TCLB_GPU && defined(__HIP_DEVICE_COMPILE__)
+  if constexpr (std::is_same<R, double>::value || std::is_same<R, float>::value) {
+    if (__builtin_amdgcn_is_shared((const void*)g)) {
+      __hip_atomic_fetch_add(g + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      return;
+    }
+  }
+#endif
+  g[i] += v;
+}
+template <class R>
+TCLB_FN void glob_max(R* g, int i, R v) {
+#if TCLB_GPU && defined(__HIP_DEVICE_COMPILE__)
+  if constexpr (std::is_same<R, double>::value || std::is_same<R, float>::value) {
+    if (__builtin_amdgcn_is_shared((const void*)g)) {
+      __hip_atomic_fetch_max(g + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      return;
+    }
+  }
+#endif
+  g[i] = g[i] > v ? g[i] : v;
+}
 
 template <class T>
 TCLB_FN T tmax(T a, T b) { return a > b ? a : b; }

@@ -42,13 +42,20 @@ __device__ __forceinline__ void atomic_max_double(double* addr, double v) {
   }
 }
 
-// Reduce per-thread accumulators g[NG] of a block and add into slot (block % TCLB_GSLOTS)
-// of dst (device, double; core.hpp TCLB_GSLOTS).  One atomic per block and global, but
-// the blocks of a launch spread over TCLB_GSLOTS addresses: with every block adding into
-// the same 8 bytes the L2 serialises ~10^5-10^6 atomics per global and launch
-// (profiles/README.md r03: the GLOB instantiations ran +25-46 % over the plain ones).
+// Globals of a block: the nodes add into the block-shared LDS accumulators acc[NG]
+// (core.hpp glob_add/glob_max: a wave reduction and one LDS atomic per AddTo call), then
+// after the barrier thread i adds acc[i] into slot (block % TCLB_GSLOTS) of dst (device,
+// double; core.hpp TCLB_GSLOTS): one atomic per block and global, spread over 64 addresses
+// per global (with every block adding into the same 8 bytes the L2 serialises ~10^5-10^6
+// atomics per global and launch; profiles/README.md r03).  The accumulators are not
+// per-thread registers, so the GLOB instantiation needs about the VGPRs of the plain one.
+#ifndef TCLB_GLOB_LDS
+#define TCLB_GLOB_LDS 1
+#endif
+// build variant "gregs" (TCLB_GLOB_LDS=0): the previous scheme, per-thread accumulators
+// g[NG] kept in registers through the node and reduced wave64 -> LDS at the end
 template <int NG, int NSUM, class R>
-__device__ __forceinline__ void block_globals(R* g, double* dst) {
+__device__ __forceinline__ void block_globals_regs(R* g, double* dst) {
   __shared__ double part[NG][16];
   const int tid = threadIdx.x + blockDim.x * threadIdx.y;
   const int lane = tid & 63, wid = tid >> 6;
@@ -68,6 +75,30 @@ __device__ __forceinline__ void block_globals(R* g, double* dst) {
       if (acc != 0.0) unsafeAtomicAdd(dst + tid, acc);
     } else {
       atomic_max_double(dst + tid, acc);
+    }
+  }
+}
+
+template <int NG, int NSUM, class R>
+__device__ __forceinline__ void block_globals_init(R* acc) {
+  const int tid = threadIdx.x + blockDim.x * threadIdx.y;
+  const int nt = blockDim.x * blockDim.y;
+  for (int i = tid; i < NG; i += nt) acc[i] = i < NSUM ? R(0) : R(-1e30);
+  __syncthreads();
+}
+template <int NG, int NSUM, class R>
+__device__ __forceinline__ void block_globals_flush(const R* acc, double* dst) {
+  __syncthreads();
+  const int tid = threadIdx.x + blockDim.x * threadIdx.y;
+  const int nt = blockDim.x * blockDim.y;
+  const unsigned b = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+  dst += (b % TCLB_GSLOTS) * (unsigned)gstride(NG);
+  for (int i = tid; i < NG; i += nt) {
+    const double a = (double)acc[i];
+    if (i < NSUM) {
+      if (a != 0.0) unsafeAtomicAdd(dst + i, a);
+    } else {
+      atomic_max_double(dst + i, a);
     }
   }
 }
@@ -96,17 +127,37 @@ template <class Model, class R, class S, int STG, bool GLOB>
 __device__ __forceinline__ void stage_body(const Launch& L) {
   const uint3 t = tile_id();
   const int x = L.xlo + (int)(t.x * blockDim.x + threadIdx.x);
-  const int y = L.ylo + (int)(t.y * blockDim.y + threadIdx.y);
+  // blockDim.x is a multiple of 64 (launch_shape), so a wave covers 64 x of one row:
+  // y is wave-uniform, and readfirstlane tells the compiler, which then keeps the row
+  // bases of every field in SGPRs (core.hpp row_at)
+  const int y = __builtin_amdgcn_readfirstlane(L.ylo + (int)(t.y * blockDim.y + threadIdx.y));
   const int z = L.zlo + (int)t.z;
-  constexpr int NG = GLOB ? Model::NGLOBALS_ : 1;
-  R g[NG];
+  if constexpr (GLOB && !TCLB_GLOB_LDS) {
+    constexpr int NG = Model::NGLOBALS_ > 0 ? Model::NGLOBALS_ : 1;
+    R g[NG];
 #pragma unroll
-  for (int i = 0; i < NG; i++) g[i] = i < Model::NSUMGLOBALS_ ? R(0) : R(-1e30);
-  if (x < L.xhi && y < L.yhi) {
-    typename Model::template NodeT<R, S, GLOB> n(L, x, y, z, g);
-    n.template run_stage<STG>();
+    for (int i = 0; i < NG; i++) g[i] = i < Model::NSUMGLOBALS_ ? R(0) : R(-1e30);
+    if (x < L.xhi && y < L.yhi) {
+      typename Model::template NodeT<R, S, GLOB> n(L, x, y, z, g);
+      n.template run_stage<STG>();
+    }
+    block_globals_regs<NG, Model::NSUMGLOBALS_>(g, L.globals);
+  } else if constexpr (GLOB) {
+    constexpr int NG = Model::NGLOBALS_ > 0 ? Model::NGLOBALS_ : 1;
+    __shared__ R acc[NG];
+    block_globals_init<NG, Model::NSUMGLOBALS_>(acc);
+    if (x < L.xhi && y < L.yhi) {
+      typename Model::template NodeT<R, S, GLOB> n(L, x, y, z, acc);
+      n.template run_stage<STG>();
+    }
+    block_globals_flush<NG, Model::NSUMGLOBALS_>(acc, L.globals);
+  } else {
+    R g[1] = {R(0)};
+    if (x < L.xhi && y < L.yhi) {
+      typename Model::template NodeT<R, S, GLOB> n(L, x, y, z, g);
+      n.template run_stage<STG>();
+    }
   }
-  if constexpr (GLOB) block_globals<NG, Model::NSUMGLOBALS_>(g, L.globals);
 }
 
 template <class Model, class R, class S, int STG, bool GLOB>
@@ -146,7 +197,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W))) k
 template <class Model, class R, class S>
 __global__ void __launch_bounds__(256) k_quantity(const Launch L) {
   const int x = L.xlo + (int)(blockIdx.x * blockDim.x + threadIdx.x);
-  const int y = L.ylo + (int)(blockIdx.y * blockDim.y + threadIdx.y);
+  const int y = __builtin_amdgcn_readfirstlane(L.ylo + (int)(blockIdx.y * blockDim.y + threadIdx.y));
   const int z = L.zlo + (int)blockIdx.z;
   if (x >= L.xhi || y >= L.yhi) return;
   R g[1];
@@ -174,7 +225,8 @@ __global__ void __launch_bounds__(64) k_sample(const Launch L, const SamplePlan 
 // Default shapes from on-device A/B (profiles/r01_tune_*): fp64 storage 128x2, fp32 256x1.
 inline void launch_shape(const Launch& L, dim3& grid, dim3& block, int sbytes = 8) {
   const int w = L.xhi - L.xlo, h = L.yhi - L.ylo, d = L.zhi - L.zlo;
-  int bx = L.block_x > 0 ? L.block_x : 0;
+  // a multiple of 64: every wave is one row segment (stage_body's wave-uniform y)
+  int bx = L.block_x > 0 ? (L.block_x + 63) / 64 * 64 : 0;
   if (bx == 0) {
     const int bmax = sbytes >= 8 ? 128 : 256;
     bx = 64;

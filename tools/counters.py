@@ -31,6 +31,9 @@ PASSES = [
     ["WRITE_SIZE", "TCC_HIT_sum", "TCC_MISS_sum"],
     ["SQ_WAVES", "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES", "SQ_INSTS_VALU", "SQ_INSTS_LDS",
      "SQ_LDS_BANK_CONFLICT", "SQ_WAIT_ANY", "SQ_ACTIVE_INST_ANY", "GRBM_GUI_ACTIVE", "GRBM_COUNT"],
+    # instruction mix and issue activity (pass 3; the raw means go to <tag>_raw.csv)
+    ["SQ_WAVES", "SQ_INSTS_VMEM_RD", "SQ_INSTS_VMEM_WR", "SQ_INSTS_SALU", "SQ_INSTS_SMEM",
+     "SQ_ACTIVE_INST_VALU", "SQ_ACTIVE_INST_VMEM", "SQ_WAIT_INST_ANY"],
 ]
 
 
@@ -119,6 +122,12 @@ def main():
                f"{mean(name, 'SQ_WAIT_ANY') / wc:.3f}" if wc == wc and wc else "nan",
                f"{clk:.2f}", s["vgpr"], s["sgpr"], s["lds"], s["scratch"]]
         lines.append(",".join(str(v) for v in row))
+    names = sorted({c for v in ctr.values() for c in v})
+    raw = [",".join(["kernel"] + names)]
+    for name in sorted(ctr):
+        raw.append(",".join([name] + [f"{mean(name, c):.6g}" for c in names]))
+    with open(os.path.join(a.outdir, f"{a.tag}_raw.csv"), "w") as f:
+        f.write("\n".join(raw) + "\n")
     text = "\n".join(lines)
     print(text)
     with open(os.path.join(a.outdir, f"{a.tag}_counters.csv"), "w") as f:
