@@ -117,6 +117,7 @@ def _adhip_source(model, gen_dir: str) -> str:
     m = model.finalize()
     src = (f"// AUTO-GENERATED: GPU adjoint (AD) executor for model {m.name}\n"
            f"#define TCLB_AD_K {ad_tangents(m)}\n"
+           f"#define TCLB_FLAT_NODE 1\n"
            f'#include "model.hpp"\n'
            f'#include "tclb_ad/executor_ad_hip.hpp"\n'
            f"TCLB_EXPORT_AD_HIP({m.name}, tclb::M_{m.name}::Model)\n")

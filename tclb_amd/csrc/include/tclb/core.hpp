@@ -230,6 +230,11 @@ struct Addr {
 // sign-extended int each access needed its own 64-bit VGPR address (two VGPRs and a
 // v_lshl_add_u64 per load; 84 of them in the pf_velocity collide).  x < 2^28: a row is
 // shorter than a field.
+// Node accessors of the emitted model header: TCLB_FLAT_NODE=1 selects one flat index per
+// access and per-thread globals (the GPU adjoint build defines it, build.py _adhip_source)
+#ifndef TCLB_FLAT_NODE
+#define TCLB_FLAT_NODE 0
+#endif
 #ifndef TCLB_ROW_ADDR
 #define TCLB_ROW_ADDR 1
 #endif
