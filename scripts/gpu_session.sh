@@ -115,6 +115,10 @@ r03o)
     step "d3q27 fp64/ms +- globals every step, variant '$v'" 400 $O/bench_glob_${v:-default}.log bash -c "TCLB_VARIANT=$v python bench.py --steps 50 && TCLB_VARIANT=$v python bench.py --steps 50 --glob-every-step && TCLB_VARIANT=$v python bench.py --steps 50 --precision mixed-shift && TCLB_VARIANT=$v python bench.py --steps 50 --precision mixed-shift --glob-every-step"
     step "pf384 fp64/ms +- globals every step, variant '$v'" 500 $O/pf384_${v:-default}.log bash -c "export TCLB_VARIANT=$v; python tools/bench_configs.py --configs pf384,cavity,part256 && python tools/bench_configs.py --configs pf384 --glob-every-step && python tools/bench_configs.py --configs pf384,cavity --precision mixed-shift && python tools/bench_configs.py --configs pf384 --precision mixed-shift --glob-every-step"
   done ;;
+pfvar)
+  for r in a b; do for v in "" nt ntld xcd; do
+    step "pf384 mixed-shift variant '$v' ($r)" 300 $O/pf384_ms_${v:-default}_$r.log env TCLB_VARIANT=$v python tools/bench_configs.py --configs pf384 --precision mixed-shift
+  done; done ;;
 pfprof)
   step "rocprof pf384 mixed-shift" 400 $O/prof_pf384_ms.log rocprofv3 --kernel-trace --stats -d $O/prof_pf384_ms -o run --output-format csv -- python3 $R/tools/bench_configs.py --configs pf384 --precision mixed-shift --steps 5 --warmup 1
   step "counters pf384 mixed-shift" 500 $O/counters_pf384_ms.log python tools/counters.py --tag pf384_mixed_shift --nodes 56623104 --outdir $O/counters -- python3 $R/tools/bench_configs.py --configs pf384 --steps 5 --warmup 1 --precision mixed-shift ;;
