@@ -119,6 +119,9 @@ pfvar)
   for r in a b; do for v in "" nt ntld xcd; do
     step "pf384 mixed-shift variant '$v' ($r)" 300 $O/pf384_ms_${v:-default}_$r.log env TCLB_VARIANT=$v python tools/bench_configs.py --configs pf384 --precision mixed-shift
   done; done ;;
+r03s)
+  step "pf384 fp64 / mixed-shift, plain and globals every step" 500 $O/pf384_glob.log bash -c 'python tools/bench_configs.py --configs pf384 && python tools/bench_configs.py --configs pf384 --glob-every-step && python tools/bench_configs.py --configs pf384 --precision mixed-shift && python tools/bench_configs.py --configs pf384 --precision mixed-shift --glob-every-step'
+  step "uncapped globals kernels: cm_cht / pf_velocity_BGK, plain and globals every step" 500 $O/heavy_glob.log bash -c 'python tools/perf_models.py --models d3q27q27_cm_cht,d3q27q7_cm_cht,d3q27_pf_velocity_BGK --n3 192 --steps 6 && python tools/perf_models.py --models d3q27q27_cm_cht,d3q27q7_cm_cht,d3q27_pf_velocity_BGK --n3 192 --steps 6 --glob-every-step' ;;
 pfprof)
   step "rocprof pf384 mixed-shift" 400 $O/prof_pf384_ms.log rocprofv3 --kernel-trace --stats -d $O/prof_pf384_ms -o run --output-format csv -- python3 $R/tools/bench_configs.py --configs pf384 --precision mixed-shift --steps 5 --warmup 1
   step "counters pf384 mixed-shift" 500 $O/counters_pf384_ms.log python tools/counters.py --tag pf384_mixed_shift --nodes 56623104 --outdir $O/counters -- python3 $R/tools/bench_configs.py --configs pf384 --steps 5 --warmup 1 --precision mixed-shift ;;

@@ -157,5 +157,7 @@ def build(outflowconvective=False, outflowneumann=False, avg=False, ibb=False, s
                  "IBB": ibb, "SMAG": smag, "CHT": cht}
     m.add_codegen(_blocks)
     m.set_dynamics(f"heat/{name}.inc")
-    m.glob_waves = 0 if outflowconvective else 2     # OutFlowConvective: 316-394 VGPRs
+    # no cap: the globals kernels sit at 256+ VGPRs, a 2-wave cap spilled 8-116 B/lane
+    # (profiles/README.md r03s); with LDS accumulators they cost what the plain ones do
+    m.glob_waves = 0
     return m

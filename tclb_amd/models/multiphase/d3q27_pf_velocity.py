@@ -295,7 +295,10 @@ def build(q27: bool = False, bgk: bool = False, thermo: bool = False, planarbenc
     m.set_dynamics("multiphase/d3q27_pf_velocity.inc")
     # GLOB kernels of the thermo / OutFlow variants need 310-370 VGPRs: a 2-wave cap would
     # spill a quarter of them; the plain pf_velocity (250-266) gains 1.5x from it
-    m.glob_waves = 0 if (thermo or outflow) else 2
+    # no occupancy cap on the globals kernels: with the accumulators in LDS they need about
+    # the VGPRs of the plain kernels (226 vs 197); a 2-wave cap made the BGK and q27
+    # variants spill 12-92 B/lane (profiles/README.md r03s)
+    m.glob_waves = 0
     return m
 
 

@@ -95,6 +95,8 @@ def build(ms=False, kl=False, trt=False, nebb=False, sup=False, singlekernel=Fal
     m.add_node_type("Solid", "BOUNDARY")
     m.add_node_type("Wall", "BOUNDARY")
     m.add_node_type("BGK", "COLLISION")
+    if singlekernel:
+        m.glob_waves = 0          # a 2-wave cap spilled its globals kernel (r03s)
     m.options = {"SEP": sep, "MS": ms, "KL": kl, "TRT": trt, "NEBB": nebb, "SUP": sup, "singlekernel": singlekernel,
                  "particles": particles}
     m.set_dynamics("particles/d3q27_psm.inc")
