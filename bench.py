@@ -47,9 +47,65 @@ def channel_flags(lat: Lattice) -> np.ndarray:
     return fl.astype(np.uint16 if m.flag_bits == 16 else np.uint32)
 
 
+def _free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def spawn_ranks(n: int, argv) -> int:
+    """--gpus N without a launcher: start N ranks of this script under
+    torch.distributed.run as a child process (nothing here has touched the GPU yet, and
+    this process never execs); rank 0's JSON line reaches our stdout through the
+    inherited descriptor.  Returns the launcher's exit code."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__), *argv]
+    return subprocess.run(cmd, env=dict(os.environ)).returncode
+
+
+def total_mass(lat: Lattice, comm) -> float:
+    """sum of every population over the lattice, in fp64 (one field at a time; the
+    *-shift storage modes keep f - w: the shift is added back per node)"""
+    nx, ny, nz = lat.shape
+    s = lat.snaps[lat.cur]
+    tot = 0.0
+    for i in range(lat.nf):
+        v = s[i, lat.gz:lat.gz + nz, lat.gy:lat.gy + ny, :nx]
+        tot += float(v.double().sum().item())
+        if lat._shift_t is not None:
+            tot += float(lat._shift_t[i, 0, 0, 0].item()) * nx * ny * nz
+    return comm.allreduce_scalar(tot, "sum")
+
+
+def physics_checks(lat: Lattice, comm, mass0: float, precision: str) -> dict:
+    """the run is physics, not noise: finite globals; total mass conserved (bounce-back
+    walls, periodic x/z, body force); and the channel's x- and z-invariance (uniform init,
+    walls only in y) holds bit for bit between the first and last x column and z plane of
+    every rank — a high-address fault or a wrong halo would break it"""
+    ok_glob = all(np.isfinite(v) for v in lat.globals.values())
+    mass1 = total_mass(lat, comm)
+    drift = abs(mass1 - mass0) / abs(mass0)
+    tol = 1e-10 if precision == "double" else 1e-5
+    nx, ny, nz = lat.shape
+    s = lat.snaps[lat.cur]
+    zinv = bool(torch.equal(s[:, lat.gz, lat.gy:lat.gy + ny, :nx], s[:, lat.gz + nz - 1, lat.gy:lat.gy + ny, :nx]))
+    xinv = bool(torch.equal(s[:, lat.gz:lat.gz + nz, lat.gy:lat.gy + ny, 0],
+                            s[:, lat.gz:lat.gz + nz, lat.gy:lat.gy + ny, nx - 1]))
+    zinv = comm.allreduce_scalar(0.0 if zinv else 1.0, "max") == 0.0
+    xinv = comm.allreduce_scalar(0.0 if xinv else 1.0, "max") == 0.0
+    ok_glob = comm.allreduce_scalar(0.0 if ok_glob else 1.0, "max") == 0.0
+    return {"globals_finite": ok_glob, "mass_rel_drift": drift, "mass_ok": bool(np.isfinite(drift) and drift <= tol),
+            "z_invariant": zinv, "x_invariant": xinv}
+
+
 def main():
+    argv = sys.argv[1:]
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None)
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--size", type=int, default=512)
@@ -64,7 +120,21 @@ def main():
                     help="globals on every step (a <Log Iterations=\"1\">-style run), not only the last")
     ap.add_argument("--loopback-dist", action="store_true",
                     help="1 rank through the multi-rank path (border/interior split + pack/unpack)")
+    ap.add_argument("--transport", default=None, choices=["rccl", "copy"],
+                    help="halo transport of --loopback-dist (rccl: RCCL send/receive to itself)")
+    ap.add_argument("--python-loop", action="store_true",
+                    help="multi-rank steps from the Python step path instead of the native loop (A/B)")
     a = ap.parse_args()
+    ws = int(os.environ.get("WORLD_SIZE", "0") or 0)
+    if ws == 0 and a.gpus is not None and a.gpus > 1:
+        sys.exit(spawn_ranks(a.gpus, argv))
+    if ws and a.gpus is not None and a.gpus != ws:
+        print(f"bench.py: --gpus {a.gpus} but the launcher started WORLD_SIZE={ws} ranks", file=sys.stderr)
+        sys.exit(2)
+    if a.transport:
+        os.environ["TCLB_DIST_TRANSPORT"] = a.transport
+    if a.python_loop:
+        os.environ["TCLB_DIST_NATIVE"] = "0"
 
     use_gpu = torch.cuda.is_available() and not a.cpu
     comm = init_distributed_from_env("cuda" if use_gpu else "cpu")
@@ -89,6 +159,7 @@ def main():
     lat.set_setting("nu", 0.02)
     lat.set_setting("ForceX", 1e-6)
     lat.init()
+    mass0 = total_mass(lat, comm)
 
     def sync():
         if use_gpu:
@@ -101,14 +172,19 @@ def main():
     if a.glob_every_step:
         for _ in range(a.steps):
             lat.iterate(1, glob_last=True)
+        t_host = time.perf_counter() - t0
     else:
-        lat.iterate(a.steps, glob_last=True)
+        lat.iterate(a.steps, glob_last=False) if a.steps > 1 else None
+        t_host = time.perf_counter() - t0       # the host's enqueue time of the window
+        lat.iterate(1, glob_last=True) if a.steps > 1 else lat.iterate(a.steps, glob_last=True)
     sync()
     dt = time.perf_counter() - t0
     dt = comm.allreduce_scalar(dt, "max")
+    t_host = comm.allreduce_scalar(t_host, "max")
     nodes = shape[0] * shape[1] * shape[2]
     mlups = nodes * a.steps / dt / 1e6
-    ok = bool(np.isfinite(lat.globals.get("XFlux", 0.0)))
+    chk = physics_checks(lat, comm, mass0, a.precision)
+    ok = chk["globals_finite"] and chk["mass_ok"] and chk["z_invariant"] and chk["x_invariant"]
     if rank == 0:
         es = lat.snaps[0].element_size()
         nf = lat.nf
@@ -133,13 +209,20 @@ def main():
                        "lattice": list(shape), "parallelism": f"zslab{world}" if world > 1 else "single",
                        "device": "cuda" if use_gpu else "cpu"},
             "effective_GBps_per_gpu": round(mlups * bytes_node / 1e3 / world, 1),
-            "globals_finite": ok,
+            "globals_finite": chk["globals_finite"],
+            "checks": chk,
+            "host_ms_per_step": round(t_host / max(1, a.steps - 1) * 1e3, 4) if not a.glob_every_step else None,
+            "loop": ("native-dist/" + lat._dist.transport) if lat._dist is not None else
+                    ("native" if lat._native_ok("Iteration") else "python"),
             "baseline_note": "reference publishes no MLUPS (BASELINE.md); vs_baseline null",
         }
         print(json.dumps(out), flush=True)
     if world > 1:
         import torch.distributed as dist
         dist.destroy_process_group()
+    if not ok:
+        print(f"bench.py: physics check failed on this run: {chk}", file=sys.stderr)
+        sys.exit(3)
 
 
 if __name__ == "__main__":

@@ -323,6 +323,29 @@ def _write_src_stamp(name: str, kind: str, variant: str, s: Optional[str] = None
             f.write(s)
 
 
+def _rt_headers() -> List[str]:
+    """headers of the native runtime libraries (not of the model libraries: an edit here
+    rebuilds libtclb_host.so / libtclb_device.so only)"""
+    d = os.path.join(CSRC, "include", "tclb_rt")
+    return [os.path.join(d, f) for f in sorted(os.listdir(d)) if f.endswith(".hpp")] + \
+        [os.path.join(CSRC, "include", "tclb", "core.hpp")]
+
+
+def host_runtime_stale() -> Optional[str]:
+    """why libtclb_host.so cannot be used as is (None: fresh)"""
+    target = os.path.join(LIB, "libtclb_host.so")
+    if not os.path.exists(target):
+        return "missing"
+    rdir = os.path.join(CSRC, "runtime")
+    srcs = sorted(os.path.join(rdir, f) for f in os.listdir(rdir) if f.endswith(".cpp"))
+    cmd = [CXX, "-O3", "-std=c++17", "-fPIC", "-shared", "-fopenmp", "-I", os.path.join(CSRC, "include"),
+           *srcs, "-lz", "-o", target + ".tmp"]
+    stamp = target + ".hash"
+    if not os.path.exists(stamp) or open(stamp).read() != _hash_inputs(srcs + _rt_headers(), " ".join(cmd)):
+        return "sources changed"
+    return None
+
+
 def build_host(force: bool = False, verbose: bool = False) -> str:
     """native host runtime library (geometry voxeliser, scans, HDF5 and PNG writers): libtclb_host.so
     from every csrc/runtime/*.cpp"""
@@ -330,8 +353,9 @@ def build_host(force: bool = False, verbose: bool = False) -> str:
     srcs = sorted(os.path.join(rdir, f) for f in os.listdir(rdir) if f.endswith(".cpp"))
     target = os.path.join(LIB, "libtclb_host.so")
     os.makedirs(LIB, exist_ok=True)
-    cmd = [CXX, "-O3", "-std=c++17", "-fPIC", "-shared", "-fopenmp", *srcs, "-lz", "-o", target + ".tmp"]
-    h = _hash_inputs(srcs, " ".join(cmd))
+    cmd = [CXX, "-O3", "-std=c++17", "-fPIC", "-shared", "-fopenmp", "-I", os.path.join(CSRC, "include"),
+           *srcs, "-lz", "-o", target + ".tmp"]
+    h = _hash_inputs(srcs + _rt_headers(), " ".join(cmd))
     stamp = target + ".hash"
     if not force and os.path.exists(target) and os.path.exists(stamp) and open(stamp).read() == h:
         return target
@@ -385,6 +409,11 @@ def bench_lib_path(name: str) -> str:
     return os.path.join(LIB, f"libtclb_{name}.so")
 
 
+def _device_cmd(srcs: List[str]) -> List[str]:
+    return [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
+            "-I", os.path.join(CSRC, "include"), *srcs, "-ldl", "-o"]
+
+
 def build_device_runtime(force: bool = False, verbose: bool = False) -> Optional[str]:
     """model-independent HIP kernels of the runtime (csrc/device/*.hip: the per-step
     particle kernels) -> _build/lib/libtclb_device.so"""
@@ -394,8 +423,8 @@ def build_device_runtime(force: bool = False, verbose: bool = False) -> Optional
     srcs = sorted(os.path.join(ddir, f) for f in os.listdir(ddir) if f.endswith(".hip"))
     target = os.path.join(LIB, "libtclb_device.so")
     os.makedirs(LIB, exist_ok=True)
-    cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", *srcs, "-o"]
-    h = _hash_inputs(srcs, " ".join(cmd))
+    cmd = _device_cmd(srcs)
+    h = _hash_inputs(srcs + _rt_headers(), " ".join(cmd))
     stamp = target + ".hash"
     if not force and os.path.exists(target) and os.path.exists(stamp) and open(stamp).read() == h:
         return target
@@ -416,11 +445,11 @@ def device_runtime_stale() -> Optional[str]:
     ddir = os.path.join(CSRC, "device")
     srcs = sorted(os.path.join(ddir, f) for f in os.listdir(ddir) if f.endswith(".hip"))
     target = os.path.join(LIB, "libtclb_device.so")
-    cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", *srcs, "-o"]
+    cmd = _device_cmd(srcs)
     if not os.path.exists(target):
         return "missing"
     stamp = target + ".hash"
-    if not os.path.exists(stamp) or open(stamp).read() != _hash_inputs(srcs, " ".join(cmd)):
+    if not os.path.exists(stamp) or open(stamp).read() != _hash_inputs(srcs + _rt_headers(), " ".join(cmd)):
         return "sources changed"
     return None
 

@@ -30,6 +30,7 @@ from .models.dsl import Model
 from .ops import abi
 from .parallel.comm import Comm, LoopbackComm
 from .parallel.decomp import Slab, decompose
+from .parallel.native import NativeDist, native_dist_enabled
 from .utils import trace
 
 _SAFE_MATH = {k: getattr(math, k) for k in ("sqrt", "exp", "log", "sin", "cos", "tan", "atan", "atan2", "pi",
@@ -156,6 +157,7 @@ class Lattice:
                           for a in ((1, 2) if ax == 3 else (ax,))}
         self.halo_lo, self.halo_hi = self.halo_sets[2 if ax == 3 else ax]
         self._halo_bufs = {}
+        self._dist = None                 # NativeDist of the native multi-rank loop (lazy)
         # native multi-step loop (ops.abi ModelLib.iterate) for halo-free lattices
         self.native_loop = (os.environ.get("TCLB_NATIVE_LOOP", "1") != "0") if native_loop is None else native_loop
         for s in m.settings:
@@ -597,7 +599,13 @@ class Lattice:
         self.run_action("Init", glob=False)
 
     def _native_ok(self, action: str) -> bool:
-        if not (self.native_loop and self.lib.has_iterate and self.g == 0 and not self.comm.distributed):
+        if not (self.native_loop and self.lib.has_iterate):
+            return False
+        if self.comm.distributed:
+            # slab-split ranks: the native multi-rank loop (parallel/native.py)
+            if not (native_dist_enabled() and NativeDist.supported(self)):
+                return False
+        elif self.g != 0:
             return False
         if self.zseries or self.callbacks or self.particles is not None or len(self.samplers) > 1:
             return False
@@ -608,8 +616,10 @@ class Lattice:
     def iterate(self, n: int, glob_last: bool = True, action: str = "Iteration", reduce: bool = True):
         """Reference Lattice::Iterate (src/Lattice.cu.Rt:900-989): globals on the last step.
 
-        Without halos, time series, callbacks or particles the n steps run in one native
-        call (tclb::iterate_action): one kernel launch per stage and no Python per step."""
+        Without time series, callbacks or particles the n steps run in one native call: on
+        one rank tclb::iterate_action (one kernel launch per stage, no Python per step), on
+        slab-split ranks the multi-rank loop of parallel/native.py (border launches, RCCL
+        exchange into the ghost planes, interior launch)."""
         if n <= 0:
             return
         if self._native_ok(action):
@@ -629,7 +639,12 @@ class Lattice:
             L.glob = self._glob_flags            # bit 0 set per step by iterate_action
             smp = self.samplers[0] if self.samplers else None
             with trace.span(f"iterate {action} x{n}"):
-                self.lib.iterate(L, self.prec, n, stages, glob_last, smp.plan_for(n) if smp else None)
+                if self.comm.distributed:
+                    if self._dist is None:
+                        self._dist = NativeDist(self)
+                    self._dist.iterate(L, self.prec, n, stages, glob_last, smp.plan_for(n) if smp else None)
+                else:
+                    self.lib.iterate(L, self.prec, n, stages, glob_last, smp.plan_for(n) if smp else None)
             if trace.SYNC:
                 trace.after_launch(self, f"{self.model.name} native loop")
             if smp:

@@ -17,7 +17,7 @@ def lib():
         if _lib is None:
             from .. import build as B
             path = os.path.join(B.LIB, "libtclb_host.so")
-            if not os.path.exists(path):
+            if B.host_runtime_stale() is not None:
                 B.build_host()
             L = ctypes.CDLL(path)
             P = ctypes.c_void_p

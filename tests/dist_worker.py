@@ -45,9 +45,10 @@ def run_case(model, shape, steps, comm, overlap=None, grid=None):
     return lat
 
 
-def worker(rank, world, port, model, shape, steps, out, overlap, grid=None):
+def worker(rank, world, port, model, shape, steps, out, overlap, grid=None, native="1"):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
+    os.environ["TCLB_DIST_NATIVE"] = native
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from tclb_amd.parallel.comm import TorchDistComm
     comm = TorchDistComm()
@@ -63,7 +64,7 @@ def worker(rank, world, port, model, shape, steps, out, overlap, grid=None):
             f.write(str(parts[0][3]))
         import json
         with open(out + ".json", "w") as f:
-            json.dump(parts[0][2], f)
+            json.dump({**parts[0][2], "_native": lat._dist.transport if lat._dist is not None else None}, f)
     dist.barrier()
     dist.destroy_process_group()
 

@@ -29,6 +29,33 @@ def test_bench_two_ranks_json_line():
     assert out["value"] > 0 and out["higher_is_better"] is True
     assert out["config"]["parallelism"] == "zslab2"
     assert out["globals_finite"] is True
+    assert out["loop"] == "native-dist/callback" and out["checks"]["z_invariant"]
     metric = base.get("metric") or base.get("headline", {}).get("metric")
     if metric:
         assert out["metric"] == metric
+
+
+def test_bench_spawns_its_own_ranks():
+    """--gpus N without a launcher starts N ranks itself (torch.distributed.run as a child
+    process): the line reports n_gpus = N, never a silent 1-rank run; the ranks step
+    through the native multi-rank loop"""
+    env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="2")
+    env.pop("WORLD_SIZE", None)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--cpu", "--gpus", "2", "--shape", "32,16,16",
+           "--steps", "3", "--warmup", "1"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["config"]["parallelism"] == "zslab2"
+    assert out["loop"] == "native-dist/callback"
+    assert all(out["checks"][k] for k in ("globals_finite", "mass_ok", "z_invariant", "x_invariant"))
+
+
+def test_bench_rejects_rank_count_mismatch():
+    env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="1", WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--cpu", "--gpus", "3", "--shape", "32,16,16",
+           "--steps", "1", "--warmup", "0"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=120, env=env, cwd=ROOT)
+    assert r.returncode == 2 and "WORLD_SIZE=2" in r.stderr

@@ -42,18 +42,45 @@ def test_model_hip_matches_cpu(name):
         assert torch.allclose(qa, qb, atol=1e-10 * s + 1e-12 * scale, rtol=1e-10), (q.name, (qa - qb).abs().max().item())
 
 
+# multi-rank step paths: the native C++ loop (parallel/native.py; on the GPU with the RCCL
+# transport sending to this rank itself, or device copies) and the Python step path
+# (halo mirror in the border kernels, or separate pack kernels)
+DIST_PATHS = {
+    "native-rccl": {"TCLB_DIST_NATIVE": "1", "TCLB_DIST_TRANSPORT": "rccl"},
+    "native-copy": {"TCLB_DIST_NATIVE": "1", "TCLB_DIST_TRANSPORT": "copy"},
+    "py-mirror": {"TCLB_DIST_NATIVE": "0", "TCLB_HALO_MIRROR": "1"},
+    "py-pack": {"TCLB_DIST_NATIVE": "0", "TCLB_HALO_MIRROR": "0"},
+}
+
+
+def _dist_env(monkeypatch, path):
+    for k, v in DIST_PATHS[path].items():
+        monkeypatch.setenv(k, v)
+
+
+def _check_path(lat, path):
+    if path.startswith("native"):
+        from tclb_amd.parallel.native import NativeDist
+        if NativeDist.supported(lat) and lat._native_ok("Iteration"):
+            want = path.split("-")[1] if lat.is_gpu else "copy"
+            assert lat._dist is not None and lat._dist.transport == want
+    else:
+        assert lat._dist is None and lat.halo_mirror == (path == "py-mirror")
+
+
 @pytest.mark.gpu
 @needs_gpu
-@pytest.mark.parametrize("mirror", ["1", "0"])
+@pytest.mark.parametrize("path", list(DIST_PATHS))
 @pytest.mark.parametrize("name", MODELS)
-def test_dist_path_on_gpu_matches_loopback(name, mirror, monkeypatch):
-    """the multi-rank step (border/interior split; border kernels writing the send
-    buffers with TCLB_HALO_MIRROR=1, separate pack kernels with 0) equals the plain
-    single-rank step bit for bit on the HIP executor, for every catalog model"""
-    monkeypatch.setenv("TCLB_HALO_MIRROR", mirror)
+def test_dist_path_on_gpu_matches_loopback(name, path, monkeypatch):
+    """the multi-rank step (border/interior split and halo exchange: native loop over RCCL
+    self send/receive or device copies; Python path with mirror or pack kernels) equals
+    the plain single-rank step bit for bit on the HIP executor, for every catalog model"""
+    _dist_env(monkeypatch, path)
     a = run(name, "cuda", steps=4, comm=LoopbackComm(exercise_dist_path=True))
     b = run(name, "cuda", steps=4, comm=LoopbackComm())
-    assert a.overlap and not b.overlap and a.halo_mirror == (mirror == "1")
+    assert a.overlap and not b.overlap
+    _check_path(a, path)
     fa, fb = a.fields_interior(), b.fields_interior()
     scale = fb.abs().max().item() + 1e-300
     # bitwise in practice; the tolerance only admits FMA-contraction differences between
@@ -61,17 +88,19 @@ def test_dist_path_on_gpu_matches_loopback(name, mirror, monkeypatch):
     assert torch.allclose(fa, fb, atol=1e-11 * scale, rtol=1e-11), (fa - fb).abs().max().item()
 
 
-@pytest.mark.parametrize("mirror", ["1", "0"])
+@pytest.mark.parametrize("path", ["native-copy", "py-mirror", "py-pack"])
 @pytest.mark.parametrize("name", MODELS)
-def test_dist_path_on_cpu_matches_loopback(name, mirror, monkeypatch):
+def test_dist_path_on_cpu_matches_loopback(name, path, monkeypatch):
     """every catalog model: the multi-rank code path with this rank as its own
-    neighbour (overlap split + halo mirror or pack/unpack) is bitwise equal to the
-    single-rank step.  Regression: a mirror buffer shared by both sides when the lo
-    and hi field lists are equal (symmetric stencils) broke 38 models."""
-    monkeypatch.setenv("TCLB_HALO_MIRROR", mirror)
+    neighbour (native loop with the halo plan as copies; Python path with halo mirror or
+    pack/unpack) is bitwise equal to the single-rank step.  Regression: a mirror buffer
+    shared by both sides when the lo and hi field lists are equal (symmetric stencils)
+    broke 38 models."""
+    _dist_env(monkeypatch, path)
     a = run(name, "cpu", steps=3, comm=LoopbackComm(exercise_dist_path=True))
     b = run(name, "cpu", steps=3, comm=LoopbackComm())
-    assert a.overlap and a.halo_mirror == (mirror == "1")
+    assert a.overlap
+    _check_path(a, path)
     assert torch.equal(a.fields_interior(), b.fields_interior())
 
 

@@ -20,22 +20,28 @@ def _port():
     return p
 
 
+@pytest.mark.parametrize("native", ["1", "0"])
 @pytest.mark.parametrize("model,shape,world,overlap", [
     ("d3q27", (16, 8, 12), 2, True),
     ("d3q27", (16, 8, 10), 3, False),
+    ("d3q27", (16, 8, 16), 4, True),
     ("d2q9", (24, 18, 1), 2, True),
 ])
-def test_ranks_match_single(tmp_path, model, shape, world, overlap):
+def test_ranks_match_single(tmp_path, model, shape, world, overlap, native):
+    """N ranks = 1 rank bit for bit, through the native multi-rank loop (native=1: C++
+    loop, halo plan executed by gloo through the loop's callback transport) and through
+    the Python step path (native=0)"""
     steps = 5
     ref = dist_worker.run_case(model, shape, steps, LoopbackComm())
     out = str(tmp_path / "full.npy")
-    mp.start_processes(dist_worker.worker, args=(world, _port(), model, shape, steps, out, overlap),
+    mp.start_processes(dist_worker.worker, args=(world, _port(), model, shape, steps, out, overlap, None, native),
                        nprocs=world, start_method="spawn", join=True)
     full = np.load(out)
     r = ref.fields_interior().numpy()
     assert full.shape == r.shape
     assert np.array_equal(full, r)
     g = json.load(open(out + ".json"))
+    assert g.pop("_native") == ("callback" if native == "1" else None)
     for k, v in ref.globals.items():
         assert abs(g[k] - v) <= 1e-11 * (1 + abs(v)), k
 
