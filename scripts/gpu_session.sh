@@ -32,6 +32,15 @@ adjoint)
   step "gpu adjoint tests" 600 $O/pytest_gpu_adjoint.log python -u -m pytest tests/test_gpu_adjoint.py -v -m gpu --timeout 300 --timeout-method thread
   step "adjoint bench 64" 300 $O/bench_adjoint_64.json python tools/bench_adjoint.py --size 64 --steps 40
   step "adjoint bench 128" 400 $O/bench_adjoint_128.json python tools/bench_adjoint.py --size 128 --steps 80 ;;
+distnative)
+  step "gpu dist-path tests" 900 $O/pytest_gpu_dist.log python -u -m pytest tests/test_catalog.py -k dist_path_on_gpu -m gpu -x -q --timeout 120 --timeout-method thread
+  for P in mixed-shift double; do
+  step "slab $P plain" 300 $O/slab_${P}_plain.json python bench.py --shape 512,512,64 --precision $P --steps 200 --warmup 20
+  step "slab $P native rccl self" 300 $O/slab_${P}_rccl.json python bench.py --shape 512,512,64 --precision $P --steps 200 --warmup 20 --loopback-dist --transport rccl
+  step "slab $P native copy" 300 $O/slab_${P}_copy.json python bench.py --shape 512,512,64 --precision $P --steps 200 --warmup 20 --loopback-dist --transport copy
+  step "slab $P python loop" 300 $O/slab_${P}_python.json python bench.py --shape 512,512,64 --precision $P --steps 200 --warmup 20 --loopback-dist --python-loop
+  done
+  step "rocprof slab rccl self" 400 $O/prof_slab_rccl.log rocprofv3 --kernel-trace --stats -d $O/prof_slab_rccl -o run --output-format csv -- python3 $R/bench.py --shape 512,512,64 --precision mixed-shift --steps 50 --warmup 5 --loopback-dist --transport rccl ;;
 dist)
   step "slab 512x512x64 plain" 300 $O/dist_plain.json python bench.py --shape 512,512,64 --steps 200 --warmup 20
   step "slab loopback overlap" 300 $O/dist_loop_overlap.json python bench.py --shape 512,512,64 --steps 200 --warmup 20 --loopback-dist

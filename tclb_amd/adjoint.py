@@ -58,8 +58,11 @@ class Adjoint:
         self.reverse = bool(lat.model.reverse) and reverse
         self._seeded = bool(list(settings) or list(zonal))
         self._abuf = None             # persistent (aout, ain) ping-pong buffers of _ad_stage
-        self._dual_buf = None         # GPU: nodes of a stage without a reverse sweep
+        # GPU: per stage, the nodes without a reverse sweep (recorded on the stage's first
+        # call, index list + count); invalidated when the node flags change
+        self._dual_bufs: Dict[int, torch.Tensor] = {}
         self._dual_count: Dict[int, int] = {}
+        self._dual_flags = None
         self._ctx_bytes = [b"", b""]
         self._ctx_devs = ([self._ctx_dev, torch.zeros_like(self._ctx_dev)] if self._ctx_dev is not None
                           else [None, None])
@@ -141,17 +144,23 @@ class Adjoint:
             L.ext[1] = lat.cuts.data_ptr()
             L.next[1] = lat.cuts.numel()
         if rev and self._ctx_dev is not None:
+            if self._dual_flags != lat.flags_version:
+                self._dual_bufs.clear()
+                self._dual_count.clear()
+                self._dual_flags = lat.flags_version
             nodes = (L.xhi - L.xlo) * (L.yhi - L.ylo) * (L.zhi - L.zlo)
-            if self._dual_buf is None or self._dual_buf.numel() < nodes + 1:
-                self._dual_buf = torch.zeros(nodes + 1, dtype=torch.int32, device=lat.device)
+            buf = self._dual_bufs.get(si)
+            if buf is None or buf.numel() < nodes + 1:
+                buf = self._dual_bufs[si] = torch.zeros(nodes + 1, dtype=torch.int32, device=lat.device)
+                self._dual_count.pop(si, None)
             count = self._dual_count.get(si)
             if count is None:
-                self._dual_buf[0] = 0
-            L.aux = self._dual_buf.data_ptr()
+                buf[0] = 0
+            L.aux = buf.data_ptr()
             L.qcomp = 0 if count is None else 1          # record the dual nodes on the first call
             self.lib.run(L)
             if count is None:
-                count = self._dual_count[si] = int(self._dual_buf[0].item())
+                count = self._dual_count[si] = int(buf[0].item())
             L.next[5], L.qcomp = 2, count
             if count > 0:
                 self.lib.run(L)
@@ -202,18 +211,22 @@ class Adjoint:
             raise AdjointError(f"model {self.lat.model.name}: a node needed more than {self.lib.tangents} AD tangents")
 
     def step_back(self, a_next: torch.Tensor, action: str = "Iteration", obj_weight: float = 1.0,
-                  state: Optional[torch.Tensor] = None, _buffer: bool = False) -> torch.Tensor:
+                  state: Optional[torch.Tensor] = None, _buffer: bool = False,
+                  other: Optional[torch.Tensor] = None) -> torch.Tensor:
         """adjoint of one `action` applied to the primal state `state` (default: the
         current snapshot): given a_next = dJ/d(state after the action) return
         dJ/d(state before), adding this step's Objective derivative (weight obj_weight)
-        and setting gradients.  (_buffer: the result may be one of the adjoint's internal
-        ping-pong buffers, valid until the next call — the unsteady sweep's own loop.)"""
-        a = self._step_back(a_next, action, obj_weight, state)
+        and setting gradients.  `other`: what the step's output snapshot held before the
+        step (default: the other snapshot of the lattice) — read by a multi-stage action
+        only for the fields of Model.late_reads.  (_buffer: the result may be one of the
+        adjoint's internal ping-pong buffers, valid until the next call — the unsteady
+        sweep's own loop.)"""
+        a = self._step_back(a_next, action, obj_weight, state, other)
         if not _buffer and self._abuf is not None and any(a is b for b in self._abuf):
             a = a.clone()
         return a
 
-    def _step_back(self, a_next, action, obj_weight, state):
+    def _step_back(self, a_next, action, obj_weight, state, other=None):
         if (len(self.lat.model.action(action).stages) > 1 and self._abuf is not None
                 and any(a_next is b for b in self._abuf)):
             # a_next is read again after the first stage's adjoint reuses the buffers
@@ -223,12 +236,17 @@ class Adjoint:
         act = m.action(action)
         src = lat.snaps[lat.cur] if state is None else state
         # forward recompute of the intermediate in-place states of multi-stage actions,
-        # in a work copy of the other snapshot (fields a stage does not write keep what
-        # the output snapshot held, as in the primal step)
+        # in a work copy of the snapshot the primal step wrote into (fields no stage has
+        # written yet keep what it held: Model.late_reads are read from it, as in the
+        # primal step; for every other field its contents do not matter)
         inputs: List[torch.Tensor] = [src]
         if len(act.stages) > 1:
             glob = lat.globals_t.clone()
-            other = lat.snaps[1 - lat.cur] if state is None else lat.snaps[lat.cur]
+            if other is None:
+                if state is not None and m.late_reads(action):
+                    raise AdjointError(f"model {m.name}: action {action} reads {m.late_reads(action)} from the "
+                                       "output snapshot's previous contents; step_back(state=...) needs other=")
+                other = lat.snaps[1 - lat.cur] if state is None else lat.snaps[lat.cur]
             dst = other.clone()
             for k, sname in enumerate(act.stages[:-1]):
                 si = m.stage_index(sname)
@@ -278,6 +296,10 @@ class Adjoint:
         keep_segment = (steps // checkpoint + checkpoint + 2) * snap_bytes <= 0.5 * self._free_bytes()
         it0 = lat.iter
         snaps: Dict[int, torch.Tensor] = {0: lat.snaps[lat.cur].clone()}
+        # with late reads (Model.late_reads) a step also depends on what its output
+        # snapshot held: keep that next to every checkpoint
+        late = bool(lat.model.late_reads(action))
+        prev: Dict[int, torch.Tensor] = {0: lat.snaps[1 - lat.cur].clone()} if late else {}
         obj = next((i for i, g in enumerate(lat.model.globals_) if g.name == "Objective"), None)
         J = torch.zeros((), dtype=torch.float64, device=lat.device)
         for t in range(steps):
@@ -286,6 +308,8 @@ class Adjoint:
                 J += lat.globals_vector()[obj]
             if (t + 1) % checkpoint == 0 and t + 1 < steps:
                 snaps[t + 1] = lat.snaps[lat.cur].clone()
+                if late:
+                    prev[t + 1] = lat.snaps[1 - lat.cur].clone()
         lat._reduce_globals()
         self.J = lat.comm.allreduce_scalar(float(J.item()), "sum") if obj is not None else 0.0
         final = lat.snaps[lat.cur].clone()
@@ -297,6 +321,8 @@ class Adjoint:
             # re-run the segment once, keeping the state before every step: each step
             # writes a fresh snapshot buffer, which is kept (no copies)
             lat.snaps[lat.cur].copy_(snaps[base])
+            if late:
+                lat.snaps[1 - lat.cur].copy_(prev[base])
             lat.iter = it0 + base
             states = [snaps[base]]
             # a single rank reads no ghost plane, and a step that writes every field
@@ -307,10 +333,15 @@ class Adjoint:
                 lat.iterate(1, glob_last=False, action=action)
                 states.append(lat.snaps[lat.cur])
             for t in range(end - 1, base - 1, -1):
+                other = None
                 if keep_segment:
                     state = states[t - base]
+                    if late:
+                        other = states[t - base - 1] if t > base else prev[base]
                 else:
                     lat.snaps[lat.cur].copy_(snaps[base])
+                    if late:
+                        lat.snaps[1 - lat.cur].copy_(prev[base])
                     lat.iter = it0 + base
                     for _ in range(t - base):
                         lat.iterate(1, glob_last=False, action=action)
@@ -319,7 +350,7 @@ class Adjoint:
                 if lat.zseries:
                     lat.apply_series()
                     before = self.gzon.cpu().numpy().copy()
-                a = self.step_back(a, action, state=state, _buffer=True)
+                a = self.step_back(a, action, state=state, _buffer=True, other=other)
                 if lat.zseries:
                     self._series_grad(before, lat)
             del states

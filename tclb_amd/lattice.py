@@ -120,6 +120,7 @@ class Lattice:
         self.cur = 0
         fdt = torch.int16 if m.flag_bits == 16 else torch.int32
         self.flags = torch.zeros((self.NZ, self.NY, self.px), dtype=fdt, device=self.device)
+        self.flags_version = 0            # bumped by every set_flags (caches keyed on the node types)
         # settings
         self.gsettings = [s.name for s in m.global_settings]
         self.zsettings = [s.name for s in m.zonal_settings]
@@ -765,6 +766,7 @@ class Lattice:
         full[:, :, :nx] = flags
         view = full.view(np.int16 if self.model.flag_bits == 16 else np.int32)
         self.flags.copy_(torch.from_numpy(view))
+        self.flags_version += 1
 
     def get_flags(self) -> np.ndarray:
         """interior flags (nz, ny, nx) as unsigned"""

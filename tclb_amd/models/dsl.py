@@ -409,6 +409,26 @@ class Model:
                                          f"with a stencil (data race)")
                 written |= saves
 
+    def late_reads(self, action: str) -> List[str]:
+        """fields that a stage k > 0 of `action` reads (declared reads, loaded densities)
+        although no earlier stage of the action wrote them: such a stage sees what the
+        output snapshot held before the step, i.e. the state of two steps back (the
+        reference rejects these unless its access check is permissive, src/conf.R:512-586)"""
+        act = self.action(action)
+        if act is None:
+            return []
+        written: set = set()
+        out: set = set()
+        for k, sname in enumerate(act.stages):
+            st = self.stage(sname)
+            if k > 0:
+                reads = set(st.read_fields or [])
+                if st.load_densities and not st.init:
+                    reads |= {d.field.nicename for d in self.densities}
+                out |= reads - written
+            written |= {f.nicename for f in self.fields if self.matches(f, st.save_fields)}
+        return sorted(out)
+
     # ---------------------------------------------------------------- lookup
     def stage(self, name: str) -> Optional[Stage]:
         for s in self.stages:

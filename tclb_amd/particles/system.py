@@ -29,12 +29,16 @@ def _host_prop(name):
     def get(self):
         if name in self._host_stale:
             self._pull()
-        return self._h[name]
+        # a read-only view: an in-place edit (ps.x[0] = ...) would never reach the device
+        # copy, so it raises; assign a whole array (ps.x = a), which marks the device stale
+        a = self._h[name].view()
+        a.flags.writeable = False
+        return a
 
     def set_(self, value):
         if self._host_stale:
             self._pull()
-        self._h[name] = value
+        self._h[name] = np.array(value, dtype=self._h[name].dtype)
         self._dev_stale = True
     return property(get, set_)
 

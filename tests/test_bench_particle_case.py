@@ -1,0 +1,28 @@
+"""The part256 benchmark case (tools/bench_configs.py) is physically stable: a density-2
+sphere in the periodic d3q19 box keeps a bounded velocity over 1 000 steps (round-3
+verdict: the previous case, rho_p/rho_f = 0.58, blew up within 50 steps and its timings
+were taken on a diverging run).  Same case shape at 64^3 on the CPU executor."""
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+
+
+def test_part256_case_stays_bounded():
+    import bench_configs as bc
+    lat = bc.part256(64, "double", torch.device("cpu"))
+    ps = lat.particles
+    assert abs(ps.m[0] / (4.0 / 3.0 * np.pi * ps.r[0] ** 3) - 2.0) < 1e-12
+    vmax = 0.0
+    for _ in range(10):
+        lat.iterate(100)
+        v = np.abs(np.asarray(ps.v)).max()
+        assert np.isfinite(v)
+        vmax = max(vmax, v)
+    assert vmax < bc.PARTICLE_VMAX, vmax
+    chk = bc.physics_checks(lat)
+    assert chk["globals_finite"] and chk["fields_finite"] and chk["particle_bounded"], chk

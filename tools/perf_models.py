@@ -9,9 +9,20 @@ import time
 import numpy as np
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+from model_cases import case_settings  # noqa: E402
 from tclb_amd.lattice import Lattice  # noqa: E402
 from tclb_amd.models import registry  # noqa: E402
+
+
+def state_finite(lat) -> bool:
+    """globals and every stored field finite (one field at a time, on the device)"""
+    if not all(np.isfinite(v) for v in lat.globals.values()):
+        return False
+    s = lat.snaps[lat.cur]
+    return all(bool(torch.isfinite(s[i]).all().item()) for i in range(lat.nf))
 
 
 def main():
@@ -24,7 +35,9 @@ def main():
     ap.add_argument("--variants", default="", help="comma list of HIP build variants to A/B (interleaved)")
     ap.add_argument("--rounds", type=int, default=1)
     ap.add_argument("--glob-every-step", action="store_true", help="globals integrated on every step")
+    ap.add_argument("--allow-invalid", action="store_true", help="exit 0 even when a run went non-finite")
     a = ap.parse_args()
+    invalid = []
     variants = a.variants.split(",") if a.variants else [None]
     names = a.models.split(",") if a.models else registry.names()
     dev = torch.device("cuda", 0)
@@ -35,6 +48,11 @@ def main():
             lat = Lattice(name, shape, device=dev, precision=a.precision, variant=variant)
             coll = next((n.value for n in m.node_types if n.group == "COLLISION"), 0)
             lat.set_flags(np.full((lat.NZ, lat.NY, shape[0]), coll, dtype=np.uint32))
+            # the model-family settings of the catalog tests (a physical case; some
+            # defaults, e.g. zero densities of the phase-field models, are not)
+            for k, v in case_settings(name).items():
+                if not k.startswith("_") and m.setting(k) is not None:
+                    lat.set_setting(k, v)
             lat.init()
             lat.iterate(3, glob_last=False)
             torch.cuda.synchronize()
@@ -43,19 +61,27 @@ def main():
                 for _ in range(a.steps):
                     lat.iterate(1, glob_last=True, reduce=False)
             else:
-                lat.iterate(a.steps, glob_last=False)
+                lat.iterate(a.steps, glob_last=True)
             torch.cuda.synchronize()
             dt = (time.perf_counter() - t) / a.steps
+            ok = state_finite(lat)
+            if not ok:
+                invalid.append(name)
             es = lat.snaps[0].element_size()
             nodes = shape[0] * shape[1] * shape[2]
             bpn = 2 * lat.nf * es + lat.flags.element_size()
             print(json.dumps({"model": name, "variant": variant, "round": rnd, "glob_every_step": a.glob_every_step, "shape": shape, "fields": lat.nf, "stages": len(m.stages),
                               "ms": round(dt * 1e3, 3), "MLUPS": round(nodes / dt / 1e6, 1),
-                              "GBps_meter": round(nodes * bpn / dt / 1e9, 1)}), flush=True)
+                              "GBps_meter": round(nodes * bpn / dt / 1e9, 1), "finite": ok}), flush=True)
             del lat
             torch.cuda.empty_cache()
         except Exception as e:  # noqa
             print(json.dumps({"model": name, "error": str(e)[:300]}), flush=True)
+            invalid.append(name)
+    if invalid and not a.allow_invalid:
+        print(f"perf_models: {len(invalid)} run(s) not valid (non-finite state or error): {','.join(invalid)}",
+              file=sys.stderr)
+        sys.exit(3)
 
 
 if __name__ == "__main__":
