@@ -50,6 +50,8 @@ VARIANTS = {
     # access instead of SGPR row base + 32-bit lane offset (core.hpp TCLB_ROW_ADDR=0)
     "gregs": ["-DTCLB_NT_STORE=1", "-DTCLB_GLOB_LDS=0"],
     "flataddr": ["-DTCLB_NT_STORE=1", "-DTCLB_ROW_ADDR=0"],
+    # A/B of the LDS-staged stencil tiles (executor_hip.hpp k_tile): global loads instead
+    "nolds": ["-DTCLB_NT_STORE=1", "-DTCLB_LDS_TILES=0"],
 }
 DEFAULT_VARIANT = os.environ.get("TCLB_VARIANT", "")
 # CPU executor variants: "ubsan" builds the node code with UndefinedBehaviorSanitizer
@@ -61,6 +63,10 @@ CPU_VARIANTS = {
 
 # GPU adjoint executor variants: tangents per pass (tclb_ad/executor_ad_hip.hpp TCLB_AD_WINDOW)
 AD_VARIANTS = {f"w{w}": [f"-DTCLB_AD_WINDOW={w}"] for w in (1, 2, 3, 5)}
+# diagnostics of the row-accessor adjoint fault (round-3 verdict, What's weak #3): the row
+# accessors of the primal build, at -O2 / -O1 / one tangent per pass
+AD_VARIANTS.update({"row": ["-DTCLB_FLAT_NODE=0"], "row_o1": ["-DTCLB_FLAT_NODE=0", "-O1"],
+                    "row_w1": ["-DTCLB_FLAT_NODE=0", "-DTCLB_AD_WINDOW=1"]})
 
 
 def _variant_of(kind: str, variant: str) -> str:
@@ -117,7 +123,7 @@ def _adhip_source(model, gen_dir: str) -> str:
     m = model.finalize()
     src = (f"// AUTO-GENERATED: GPU adjoint (AD) executor for model {m.name}\n"
            f"#define TCLB_AD_K {ad_tangents(m)}\n"
-           f"#define TCLB_FLAT_NODE 1\n"
+           f"#ifndef TCLB_FLAT_NODE\n#define TCLB_FLAT_NODE 1\n#endif\n"
            f'#include "model.hpp"\n'
            f'#include "tclb_ad/executor_ad_hip.hpp"\n'
            f"TCLB_EXPORT_AD_HIP({m.name}, tclb::M_{m.name}::Model)\n")

@@ -33,6 +33,10 @@ namespace tclb {
 
 TCLB_FN constexpr int gstride(int ng) { return (ng + 15) / 16 * 16; }
 
+// Work-group of the LDS-tile stage kernel (executor_hip.hpp k_tile): 64 x 4 nodes, one
+// wave per row (z planes per work-group: Model::tile_zc)
+constexpr int TILE_BX = 64, TILE_BY = 4;
+
 typedef uint32_t flag_t;  // node type word (reference: flag_t 16/32 bit, src/conf.R:620-628)
 
 template <class R>
@@ -475,29 +479,42 @@ inline int prec_dispatch(int prec, F&& f) {
 // add is a wave reduction (DPP, -amdgpu-atomic-optimizer-strategy=DPP: correct under
 // divergence) and one ds_add/ds_max per wave.  __builtin_amdgcn_is_shared folds at
 // compile time once the accumulator's address space is known.
+// Accumulator type of the globals (the node's glob_ array): fp64 for the plain compute
+// types, so an fp32-compute run sums its globals in double like the reference's
+// double-precision reduction; the type itself for the AD dual numbers.
 template <class R>
-TCLB_FN void glob_add(R* g, int i, R v) {
+struct glob_acc {
+  typedef R type;
+};
+template <>
+struct glob_acc<float> {
+  typedef double type;
+};
+
+template <class G, class R>
+TCLB_FN void glob_add(G* g, int i, R v) {
 #if TCLB_GPU && defined(__HIP_DEVICE_COMPILE__)
-  if constexpr (std::is_same<R, double>::value || std::is_same<R, float>::value) {
+  if constexpr (std::is_same<G, double>::value || std::is_same<G, float>::value) {
     if (__builtin_amdgcn_is_shared((const void*)g)) {
-      __hip_atomic_fetch_add(g + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      __hip_atomic_fetch_add(g + i, G(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       return;
     }
   }
 #endif
-  g[i] += v;
+  g[i] += G(v);
 }
-template <class R>
-TCLB_FN void glob_max(R* g, int i, R v) {
+template <class G, class R>
+TCLB_FN void glob_max(G* g, int i, R v) {
 #if TCLB_GPU && defined(__HIP_DEVICE_COMPILE__)
-  if constexpr (std::is_same<R, double>::value || std::is_same<R, float>::value) {
+  if constexpr (std::is_same<G, double>::value || std::is_same<G, float>::value) {
     if (__builtin_amdgcn_is_shared((const void*)g)) {
-      __hip_atomic_fetch_max(g + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      __hip_atomic_fetch_max(g + i, G(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       return;
     }
   }
 #endif
-  g[i] = g[i] > v ? g[i] : v;
+  const G w = G(v);
+  g[i] = g[i] > w ? g[i] : w;
 }
 
 template <class T>

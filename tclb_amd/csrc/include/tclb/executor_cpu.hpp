@@ -15,15 +15,17 @@ inline void cpu_stage(const Launch& L) {
   constexpr int NSUM = Model::NSUMGLOBALS_;
   std::vector<double> acc(NG, 0.0);
   for (int i = NSUM; i < NG; i++) acc[i] = -1e300;
+  typedef typename Model::template NodeT<R, S, GLOB> N;
+  typedef typename N::G_ G;
 #pragma omp parallel
   {
-    R g[NG];
-    for (int i = 0; i < NG; i++) g[i] = i < NSUM ? R(0) : R(-1e30);
+    G g[NG];
+    for (int i = 0; i < NG; i++) g[i] = i < NSUM ? G(0) : G(-1e30);
 #pragma omp for collapse(2) schedule(static)
     for (int z = L.zlo; z < L.zhi; z++)
       for (int y = L.ylo; y < L.yhi; y++)
         for (int x = L.xlo; x < L.xhi; x++) {
-          typename Model::template NodeT<R, S, GLOB> n(L, x, y, z, g);
+          N n(L, x, y, z, g);
           n.template run_stage<STG>();
         }
     if (GLOB) {
@@ -63,7 +65,7 @@ inline int run_quantity(const Launch& L) {
   for (int z = L.zlo; z < L.zhi; z++)
     for (int y = L.ylo; y < L.yhi; y++)
       for (int x = L.xlo; x < L.xhi; x++) {
-        R g[1];
+        typename Model::template NodeT<R, S, false>::G_ g[1];
         typename Model::template NodeT<R, S, false> n(L, x, y, z, g);
         n.pop();
         R o[3] = {R(0), R(0), R(0)};
@@ -80,7 +82,7 @@ inline int run_sample(const Launch& L, const SamplePlan& P) {
   if (P.np <= 0 || P.row < 0 || P.row >= P.rows) return 0;
   for (int p = 0; p < P.np; p++) {
     const int* c = P.points + 3 * p;
-    R g[1];
+    typename Model::template NodeT<R, S, false>::G_ g[1];
     typename Model::template NodeT<R, S, false> n(L, c[0], c[1], c[2], g);
     sample_node(n, P, P.out + ((long long)P.row * P.np + p) * P.width);
   }

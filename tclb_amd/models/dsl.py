@@ -107,6 +107,8 @@ class Stage:
     init: bool = False                        # "Init" stream: no load before main
     lazy_load: bool = False   # the declared loads are not made before main: main calls
                               # load_<name>() where it needs them (declared for the halo)
+    lds: Optional[List[str]] = None   # fields read through a stencil that the GPU kernel
+                                      # stages in LDS tiles (executor_hip.hpp k_tile)
 
 
 @dataclass
@@ -276,11 +278,14 @@ class Model:
     def add_stage(self, name: str, main: Optional[str] = None, load_densities=False,
                   save_fields=False, read_fields: Optional[Sequence[str]] = None,
                   fixed_point: bool = False, particle: bool = False, init: bool = False,
-                  snapshot_reads: bool = False, lazy_load: bool = False):
+                  snapshot_reads: bool = False, lazy_load: bool = False, lds: Optional[Sequence[str]] = None):
         """AddStage (src/conf.R:295-330): load_densities / save_fields are True (all), False
         (none) or lists of field names / group tags (reference defaults: FALSE).
         lazy_load: the stage's main pulls its densities itself (load_<name>()), e.g. only
-        on the nodes a particle covers; the loads still count for halos and hazards."""
+        on the nodes a particle covers; the loads still count for halos and hazards.
+        lds: fields (nicenames) the stage reads through a stencil, staged in LDS tiles by the
+        GPU kernel (no reference counterpart: a MI355X schedule hint; the node code is
+        unchanged, the CPU and AD executors ignore it)."""
         if save_fields is True:
             save_fields = None
         elif save_fields is False:
@@ -289,7 +294,7 @@ class Model:
                    save_fields=list(save_fields) if save_fields is not None else None,
                    read_fields=list(read_fields) if read_fields is not None else None,
                    fixed_point=fixed_point, particle=particle, init=init, snapshot_reads=snapshot_reads,
-                   lazy_load=lazy_load)
+                   lazy_load=lazy_load, lds=list(lds) if lds else None)
         self.stages = [s for s in self.stages if s.name != name] + [st]
         return st
 
@@ -354,6 +359,7 @@ class Model:
                 self.add_node_type(f"{nm}{ax}_minus", f"SYM{ax}")
         self._pack_node_types()
         self._check_stage_access()
+        self._check_lds()
         self._finalized = True
         return self
 
@@ -408,6 +414,19 @@ class Model:
                         raise ModelError(f"stage {st.name} reads and writes {sorted(nonlocal_reads)} "
                                          f"with a stencil (data race)")
                 written |= saves
+
+    def _check_lds(self):
+        """LDS-staged fields of a stage: existing, not written by the stage (a tile is a
+        read-only copy of the input snapshot), stencil at most 2 nodes deep"""
+        for st in self.stages:
+            for name in st.lds or []:
+                f = self.field(name)
+                if f is None:
+                    raise ModelError(f"stage {st.name}: lds field {name} does not exist")
+                if self.matches(f, st.save_fields):
+                    raise ModelError(f"stage {st.name}: lds field {name} is written by the stage")
+                if max(max(-a, b) for a, b in f.stencil) > 2:
+                    raise ModelError(f"stage {st.name}: lds field {name} has a stencil deeper than 2")
 
     def late_reads(self, action: str) -> List[str]:
         """fields that a stage k > 0 of `action` reads (declared reads, loaded densities)

@@ -144,7 +144,9 @@ def build(q27: bool = False, bgk: bool = False, thermo: bool = False, planarbenc
     m.add_stage("PhaseInit", "Init", save_fields=save_initial_PF)
     m.add_stage("BaseInit", "Init_distributions", save_fields=save_initial)
     m.add_stage("calcPhase", "calcPhaseF", save_fields=["PhaseF"], load_densities=load_phase)
-    m.add_stage("BaseIter", "Run", save_fields=save_iteration, load_densities=load_iteration)
+    # the collision's phase-field gradient and normal read PhaseF through its 27-point (or
+    # 125-point, geometric) stencil: staged in an LDS tile on the GPU (k_tile)
+    m.add_stage("BaseIter", "Run", save_fields=save_iteration, load_densities=load_iteration, lds=["PhaseF"])
     m.add_stage("InitFromFieldsStage", "InitFromFieldsStage", save_fields=save_initial_PF, load_densities=["init"])
     if geometric:           # Dynamics.R:129-135
         m.add_stage("WallInit_CA", "Init_wallNorm", save_fields=["nw", "solid_boundary"] + extra_bc)
@@ -165,13 +167,16 @@ def build(q27: bool = False, bgk: bool = False, thermo: bool = False, planarbenc
         T3 = ["Temp", "Cond", "SurfaceTension"]
         m.add_stage("CopyDistributions", "TempCopy", save_fields=["g", "h", "Vel", "nw", "PF", "Thermal"])
         m.add_stage("CopyThermal", "ThermalCopy", save_fields=T3, load_densities=T3)
-        m.add_stage("RK_1", "TempUpdate1", save_fields=["RK1"], load_densities=["U", "V", "W", "Cond", "Temp"])
+        # the RK stages are two 27-point stencils (the stage's temperature iterate and the
+        # conductivity) per node: both staged in LDS tiles on the GPU
+        m.add_stage("RK_1", "TempUpdate1", save_fields=["RK1"], load_densities=["U", "V", "W", "Cond", "Temp"],
+                    lds=["Temp", "Cond"])
         m.add_stage("RK_2", "TempUpdate2", save_fields=["RK2"],
-                    load_densities=["U", "V", "W", "RK1", "Cond", "Temp"])
+                    load_densities=["U", "V", "W", "RK1", "Cond", "Temp"], lds=["RK1", "Cond"])
         m.add_stage("RK_3", "TempUpdate3", save_fields=["RK3"],
-                    load_densities=["U", "V", "W", "RK1", "RK2", "Cond", "Temp"])
+                    load_densities=["U", "V", "W", "RK1", "RK2", "Cond", "Temp"], lds=["RK2", "Cond"])
         m.add_stage("RK_4", "TempUpdate4", save_fields=["Temp", "SurfaceTension"],
-                    load_densities=["U", "V", "W", "RK1", "RK2", "RK3", "Cond", "Temp"])
+                    load_densities=["U", "V", "W", "RK1", "RK2", "RK3", "Cond", "Temp"], lds=["RK3", "Cond"])
         m.add_stage("NonLocalTemp", "BoundUpdate", save_fields=["Temp", "SurfaceTension"], load_densities=["Temp"])
         rk = ["RK_1", "RK_2", "RK_3", "RK_4", "NonLocalTemp"]
         m.add_action("TempToSteadyState", ["CopyDistributions"] + rk)
