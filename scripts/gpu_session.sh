@@ -37,9 +37,9 @@ addiag)
     step "adjoint diag ${V:-flat}" 300 $O/adjoint_diag_${V:-flat}.jsonl env TCLB_AD_VARIANT=$V TCLB_NO_BUILD=1 python tools/adjoint_diag.py --repeats 2
   done ;;
 tiles)
-  step "pf thermo 256 fp64 tiles vs nolds" 600 $O/tiles_thermo_256_fp64.jsonl python tools/perf_models.py --models d3q27_pf_velocity_thermo --n3 256 --steps 20 --variants ",nolds" --rounds 2
-  step "pf 384 fp64 tiles vs nolds" 600 $O/tiles_pf384_fp64.jsonl python tools/perf_models.py --models d3q27_pf_velocity --n3 384 --steps 20 --variants ",nolds" --rounds 2
-  step "pf 384 mixed-shift tiles vs nolds" 600 $O/tiles_pf384_ms.jsonl python tools/perf_models.py --models d3q27_pf_velocity --n3 384 --steps 20 --precision mixed-shift --variants ",nolds" --rounds 2
+  step "pf thermo 256 fp64 tiles vs nolds" 600 $O/tiles_thermo_256_fp64.jsonl python tools/perf_models.py --models d3q27_pf_velocity_thermo --n3 256 --steps 20 --variants ",nolds" --rounds 2 --allow-invalid
+  step "pf 384 fp64 tiles vs nolds" 600 $O/tiles_pf384_fp64.jsonl python tools/perf_models.py --models d3q27_pf_velocity --n3 384 --steps 20 --variants ",nolds" --rounds 2 --allow-invalid
+  step "pf 384 mixed-shift tiles vs nolds" 600 $O/tiles_pf384_ms.jsonl python tools/perf_models.py --models d3q27_pf_velocity --n3 384 --steps 20 --precision mixed-shift --variants ",nolds" --rounds 2 --allow-invalid
   step "rocprof pf thermo 256" 400 $O/prof_thermo.log rocprofv3 --kernel-trace --stats -d $O/prof_thermo -o run --output-format csv -- python3 $R/tools/perf_models.py --models d3q27_pf_velocity_thermo --n3 256 --steps 10 ;;
 gputests) step "gpu tests" 1100 $O/pytest_gpu.log python -u -m pytest tests -q -m gpu --maxfail=30 --timeout 120 --timeout-method thread -p no:cacheprovider ;;
 distnative)

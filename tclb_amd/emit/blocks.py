@@ -116,6 +116,22 @@ def exprs_function(fname: str, args: Sequence[str], exprs: Sequence[sp.Expr], ou
     return "\n".join([head, body, "  }"])
 
 
+def vjp_function(fname: str, args: Sequence[str], exprs: Sequence[sp.Expr]) -> str:
+    """Transposed Jacobian-vector product of a block of expressions, for hand-written
+    reverse sweeps (Model.set_reverse): out[j] = sum_i a[i] * d exprs[i] / d args[j].
+    The reference gets these from Tapenade's reverse mode over the generated C
+    (tools/makeAD); here they are differentiated symbolically at build time."""
+    syms = [sp.Symbol(a) for a in args]
+    a = [sp.Symbol(f"adj_{i}") for i in range(len(exprs))]
+    outs = [sp.expand(sum(a[i] * sp.diff(sp.sympify(e), s) for i, e in enumerate(exprs))) for s in syms]
+    rename = {a[i]: f"a[{i}]" for i in range(len(exprs))}
+    arglist = ", ".join(f"R {x}" for x in args)
+    head = f"  TCLB_FN static void {fname}({arglist}, const R* a, R* out) {{"
+    body = assign_block([f"out[{k}]" for k in range(len(syms))], outs, rename=rename, indent="    ",
+                        tmp_prefix="v_")
+    return "\n".join([head, body, "  }"])
+
+
 def feq_block(fname: str, U, order: int = 2) -> str:
     """Equilibrium of a velocity set U in the reference's raw-moment (product-form,
     J-truncated) construction, MRT_eq(U, rho, J)$feq (src/lib/feq.R:38-82):

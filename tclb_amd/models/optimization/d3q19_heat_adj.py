@@ -13,7 +13,7 @@ import numpy as np
 import sympy as sp
 
 from ..dsl import Model
-from ...emit.blocks import dense_transform, exprs_function
+from ...emit.blocks import dense_transform, exprs_function, vjp_function
 from ...emit.symbolic import d3q19_mrtmat, d3q19_velocities, mrt_eq_mat
 
 U7 = np.array([[0, 0, 0], [1, 0, 0], [-1, 0, 0], [0, 1, 0], [0, -1, 0], [0, 0, 1], [0, 0, -1]])
@@ -36,6 +36,12 @@ def _blocks(_m):
         out.append(exprs_function(f"{pre}_feq", ["rho", "Jx", "Jy", "Jz"], eq.feq))
         ords = ", ".join(str(int(o)) for o in eq.order)
         out.append(f"  TCLB_FN static constexpr int {pre}_order(int k) {{ constexpr int o[{n}] = {{{ords}}}; return o[k]; }}")
+        # transposes for the reverse sweep (rev_run): linear maps and the Jacobians of the
+        # equilibria in (rho, J)
+        out.append(dense_transform(f"{pre}_moments_T", eq.mat.T, n, n, "a_f = a_m . MAT^T"))
+        out.append(dense_transform(f"{pre}_inverse_T", eq.mat.inv().T, n, n, "a_m = a_f . (MAT^-1)^T"))
+        out.append(vjp_function(f"{pre}_req_T", ["rho", "Jx", "Jy", "Jz"], eq.Req))
+        out.append(vjp_function(f"{pre}_feq_T", ["rho", "Jx", "Jy", "Jz"], eq.feq))
     return "\n".join(out)
 
 
@@ -82,4 +88,5 @@ def build() -> Model:
     m.add_node_type("Outlet", "OBJECTIVE")
     m.add_codegen(_blocks)
     m.set_dynamics("optimization/d3q19_heat_adj.inc")
+    m.set_reverse("Run", "rev_ok_run", "rev_run")
     return m

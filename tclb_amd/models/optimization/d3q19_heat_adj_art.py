@@ -23,7 +23,10 @@ U7 = np.array([[0, 0, 0], [1, 0, 0], [-1, 0, 0], [0, 1, 0], [0, -1, 0], [0, 0, 1
 def _blocks(_m):
     M = d3q19_mrtmat()
     return "\n".join([dense_transform("art_moments", M, 19, 19, "moments = f . MRTMAT"),
-                      dense_transform("art_inverse", M.inv(), 19, 19, "f = moments . MRTMAT^-1")])
+                      dense_transform("art_inverse", M.inv(), 19, 19, "f = moments . MRTMAT^-1"),
+                      # transposes for the reverse sweep (heat_adj_art_common.inc art_rev_collide)
+                      dense_transform("art_moments_T", M.T, 19, 19, "a_f = a_m . MRTMAT^T"),
+                      dense_transform("art_inverse_T", M.inv().T, 19, 19, "a_m = a_f . (MRTMAT^-1)^T")])
 
 
 def build() -> Model:
@@ -71,4 +74,5 @@ def build() -> Model:
     m.add_node_type("DesignSpace", "DESIGNSPACE")
     m.add_codegen(_blocks)
     m.set_dynamics("optimization/d3q19_heat_adj_art.inc")
+    m.set_reverse("Run", "rev_ok_run", "rev_run")
     return m

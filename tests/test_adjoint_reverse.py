@@ -76,3 +76,131 @@ def test_seeded_setting_uses_dual_passes():
 def test_reverse_sweep_matches_dual_gpu():
     r = _check("cuda")
     assert r.lib.kind == "adhip" if hasattr(r.lib, "kind") else True
+
+
+# ---------------------------------------------------------------- d3q19_heat_adj
+def _heat_case(device, reverse, steps=8):
+    """heat-exchanger lattice: walls, MRT fluid with heaters, thermometers, an outlet plane,
+    a design block, a BGK and a flag-free node; every objective weight on"""
+    nx, ny, nz = 12, 7, 6
+    lat = Lattice("d3q19_heat_adj", (nx, ny, nz), device=torch.device(device))
+    m = lat.model
+    mrt = m.node_type("MRT").value
+    fl = np.full((lat.NZ, lat.NY, nx), mrt, dtype=np.uint32)
+    fl[:, 0, :] = m.node_type("Wall").value
+    fl[:, ny - 1, :] = m.node_type("Wall").value
+    fl[:, 1:3, 3] |= m.node_type("Heater").value
+    fl[:, 3, 6] |= m.node_type("Thermometer").value
+    fl[:, 4, 7] |= m.node_type("Thermometer").value
+    fl[:, 1:ny - 1, 9] |= m.node_type("Outlet").value
+    fl[:, 2:5, 4:6] |= m.node_type("DesignSpace").value
+    fl[1, 3, 10] = m.node_type("BGK").value
+    fl[2, 3, 10] = 0
+    lat.set_flags(fl)
+    for k, v in {"nu": 0.1, "FluidAlpha": 0.08, "Velocity": 0.02, "Temperature": 1.3, "LimitTemperature": 1.05,
+                 "FluxInObj": 0.4, "HeatFluxInObj": 1.0, "HeatSquareFluxInObj": -0.3,
+                 "TemperatureAtPointInObj": 0.6, "HighTemperatureInObj": 2.0, "LowTemperatureInObj": 0.7,
+                 "MaterialPenaltyInObj": 0.05}.items():
+        lat.set_setting(k, v)
+    lat.init()
+    f = lat.fields_interior().clone()
+    g = torch.Generator().manual_seed(3)
+    f = f * (1 + 0.02 * torch.rand(f.shape, generator=g, dtype=f.dtype)).to(f.device)
+    wi = m.field_index("w")
+    f[wi] = (0.4 + 0.5 * torch.rand(f[wi].shape, generator=g, dtype=f.dtype)).to(f.device)
+    lat.set_fields_interior(f)
+    ad = Adjoint(lat, reverse=reverse)
+    ad.unsteady(steps)
+    return lat, ad
+
+
+def _check_heat(device):
+    lat_r, r = _heat_case(device, True)
+    lat_d, d = _heat_case(device, False)
+    a, b = r.a0.cpu(), d.a0.cpu()
+    scale = b.abs().max().item()
+    assert scale > 0
+    assert torch.allclose(a, b, rtol=0, atol=1e-12 * scale), (a - b).abs().max().item() / scale
+    assert abs(r.J - d.J) <= 1e-13 * abs(d.J)
+    gw_r, gw_d = r.field_gradient("w"), d.field_gradient("w")
+    assert np.abs(gw_d).max() > 0
+    np.testing.assert_allclose(gw_r, gw_d, rtol=0, atol=1e-12 * np.abs(gw_d).max())
+    return r
+
+
+def test_heat_reverse_sweep_matches_dual_cpu():
+    """d3q19_heat_adj rev_run (emitter-differentiated equilibria, transposed moment
+    maps) = the dual-number adjoint of Run, every node type"""
+    _check_heat("cpu")
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not torch.cuda.is_available(), reason="no GPU")
+def test_heat_reverse_sweep_matches_dual_gpu():
+    _check_heat("cuda")
+
+
+# ---------------------------------------------------------------- d3q19_heat_adj_art
+def _art_case(device, reverse, steps=8):
+    """article heat exchanger: W velocity / pressure inlets, a limited-pressure node and an
+    E outlet (dual passes), walls, heaters, thermometers, outlet plane, design block"""
+    nx, ny, nz = 12, 7, 6
+    lat = Lattice("d3q19_heat_adj_art", (nx, ny, nz), device=torch.device(device))
+    m = lat.model
+    mrt = m.node_type("MRT").value
+    fl = np.full((lat.NZ, lat.NY, nx), mrt, dtype=np.uint32)
+    fl[:, 0, :] = m.node_type("Wall").value
+    fl[:, ny - 1, :] = m.node_type("Wall").value
+    fl[:, 1:4, 0] = m.node_type("WVelocity").value | mrt
+    fl[:, 4:ny - 1, 0] = m.node_type("WPressure").value | mrt
+    fl[:, 3, 0] = m.node_type("WPressureL").value | mrt
+    fl[:, 1:ny - 1, nx - 1] = m.node_type("EPressure").value | mrt
+    fl[:, 1:3, 3] |= m.node_type("Heater").value
+    fl[:, 3, 6] |= m.node_type("Thermometer").value
+    fl[:, 4, 7] |= m.node_type("Thermometer").value
+    fl[:, 1:ny - 1, 9] |= m.node_type("Outlet").value
+    fl[:, 2:5, 4:6] |= m.node_type("DesignSpace").value
+    fl[1, 3, 10] = m.node_type("BGK").value
+    fl[2, 3, 10] = 0
+    lat.set_flags(fl)
+    for k, v in {"nu": 0.1, "FluidAlpha": 0.08, "SolidAlpha": 0.02, "Velocity": 0.02, "Pressure": 0.003,
+                 "Temperature": 1.3, "LimitTemperature": 1.05, "FluxInObj": 0.4, "HeatFluxInObj": 1.0,
+                 "HeatSquareFluxInObj": -0.3, "TemperatureAtPointInObj": 0.6, "HighTemperatureInObj": 2.0,
+                 "LowTemperatureInObj": 0.7, "HeatInputInObj": 0.25, "MaterialPenaltyInObj": 0.05}.items():
+        lat.set_setting(k, v)
+    lat.init()
+    f = lat.fields_interior().clone()
+    g = torch.Generator().manual_seed(4)
+    f = f * (1 + 0.02 * torch.rand(f.shape, generator=g, dtype=f.dtype)).to(f.device)
+    wi = m.field_index("w")
+    f[wi] = (0.4 + 0.5 * torch.rand(f[wi].shape, generator=g, dtype=f.dtype)).to(f.device)
+    lat.set_fields_interior(f)
+    ad = Adjoint(lat, reverse=reverse)
+    ad.unsteady(steps)
+    return lat, ad
+
+
+def _check_art(device):
+    lat_r, r = _art_case(device, True)
+    lat_d, d = _art_case(device, False)
+    a, b = r.a0.cpu(), d.a0.cpu()
+    scale = b.abs().max().item()
+    assert scale > 0
+    assert torch.allclose(a, b, rtol=0, atol=1e-12 * scale), (a - b).abs().max().item() / scale
+    assert abs(r.J - d.J) <= 1e-13 * abs(d.J)
+    gw_r, gw_d = r.field_gradient("w"), d.field_gradient("w")
+    assert np.abs(gw_d).max() > 0
+    np.testing.assert_allclose(gw_r, gw_d, rtol=0, atol=1e-12 * np.abs(gw_d).max())
+    return r
+
+
+def test_art_reverse_sweep_matches_dual_cpu():
+    """d3q19_heat_adj_art rev_run (collision transpose + probed affine inlets/walls; the
+    limited inlet and the outlet on dual passes) = the dual-number adjoint"""
+    _check_art("cpu")
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not torch.cuda.is_available(), reason="no GPU")
+def test_art_reverse_sweep_matches_dual_gpu():
+    _check_art("cuda")
