@@ -41,4 +41,5 @@ def build() -> Model:
     m.add_node_type("MRT", "COLLISION")
     m.add_node_type("DesignSpace", "DESIGNSPACE")
     m.set_dynamics("optimization/d2q9_adj.inc")
+    m.set_reverse("Run", "rev_ok_run", "rev_run")
     return m

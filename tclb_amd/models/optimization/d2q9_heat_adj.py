@@ -49,4 +49,5 @@ def build() -> Model:
     m.add_node_type("MRT", "COLLISION")
     m.add_node_type("Outlet", "OBJECTIVE")
     m.set_dynamics("optimization/d2q9_heat_adj.inc")
+    m.set_reverse("Run", "rev_ok_run", "rev_run")
     return m

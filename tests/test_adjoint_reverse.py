@@ -204,3 +204,129 @@ def test_art_reverse_sweep_matches_dual_cpu():
 @pytest.mark.skipif(not torch.cuda.is_available(), reason="no GPU")
 def test_art_reverse_sweep_matches_dual_gpu():
     _check_art("cuda")
+
+
+# ---------------------------------------------------------------- d2q9_adj
+def _d2q9_case(device, reverse, steps=10):
+    """porous channel: W velocity / pressure inlets, E pressure / velocity outlets, walls,
+    solid, BGK and flag-free nodes, inlet / outlet objective planes, a design block"""
+    nx, ny = 16, 10
+    lat = Lattice("d2q9_adj", (nx, ny, 1), device=torch.device(device))
+    m = lat.model
+    mrt = m.node_type("MRT").value
+    fl = np.full((lat.NZ, lat.NY, nx), mrt, dtype=np.uint32)
+    fl[:, 0, :] = m.node_type("Wall").value
+    fl[:, ny - 1, :] = m.node_type("Wall").value
+    fl[:, 1:5, 0] = m.node_type("WVelocity").value | mrt
+    fl[:, 5:ny - 1, 0] = m.node_type("WPressure").value | mrt
+    fl[:, 1:6, nx - 1] = m.node_type("EPressure").value | mrt
+    fl[:, 6:ny - 1, nx - 1] = m.node_type("EVelocity").value | mrt
+    fl[:, 1:ny - 1, 2] |= m.node_type("Inlet").value
+    fl[:, 1:ny - 1, 12] |= m.node_type("Outlet").value
+    fl[:, 3:7, 5:9] |= m.node_type("DesignSpace").value
+    fl[:, 4, 10] = m.node_type("Solid").value | mrt
+    fl[:, 5, 10] = m.node_type("BGK").value
+    fl[:, 6, 10] = 0
+    lat.set_flags(fl)
+    for k, v in {"nu": 0.1, "Velocity": 0.02, "Pressure": 0.002, "ForceX": 1e-5, "ForceY": -2e-6,
+                 "PorocityTheta": -1.2, "DragInObj": 0.3, "LiftInObj": -0.2, "MaterialPenaltyInObj": 0.05,
+                 "MaterialInObj": 0.02, "PressureLossInObj": 1.0, "OutletFluxInObj": 0.5,
+                 "InletFluxInObj": -0.4}.items():
+        lat.set_setting(k, v)
+    lat.init()
+    f = lat.fields_interior().clone()
+    g = torch.Generator().manual_seed(6)
+    f = f * (1 + 0.02 * torch.rand(f.shape, generator=g, dtype=f.dtype)).to(f.device)
+    wi = m.field_index("w")
+    f[wi] = (0.4 + 0.5 * torch.rand(f[wi].shape, generator=g, dtype=f.dtype)).to(f.device)
+    lat.set_fields_interior(f)
+    ad = Adjoint(lat, reverse=reverse)
+    ad.unsteady(steps)
+    return lat, ad
+
+
+def _check_d2q9(device):
+    lat_r, r = _d2q9_case(device, True)
+    lat_d, d = _d2q9_case(device, False)
+    a, b = r.a0.cpu(), d.a0.cpu()
+    scale = b.abs().max().item()
+    assert scale > 0
+    assert torch.allclose(a, b, rtol=0, atol=1e-12 * scale), (a - b).abs().max().item() / scale
+    assert abs(r.J - d.J) <= 1e-13 * abs(d.J)
+    gw_r, gw_d = r.field_gradient("w"), d.field_gradient("w")
+    assert np.abs(gw_d).max() > 0
+    np.testing.assert_allclose(gw_r, gw_d, rtol=0, atol=1e-12 * np.abs(gw_d).max())
+    return r
+
+
+def test_d2q9_adj_reverse_sweep_matches_dual_cpu():
+    """d2q9_adj rev_run (hand-transposed porous MRT collision, probed Zou/He planes and
+    bounce-back) = the dual-number adjoint, every node type"""
+    _check_d2q9("cpu")
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not torch.cuda.is_available(), reason="no GPU")
+def test_d2q9_adj_reverse_sweep_matches_dual_gpu():
+    _check_d2q9("cuda")
+
+
+# ---------------------------------------------------------------- d2q9_heat_adj
+def _d2q9_heat_case(device, reverse, steps=10):
+    nx, ny = 16, 10
+    lat = Lattice("d2q9_heat_adj", (nx, ny, 1), device=torch.device(device))
+    m = lat.model
+    mrt = m.node_type("MRT").value
+    fl = np.full((lat.NZ, lat.NY, nx), mrt, dtype=np.uint32)
+    fl[:, 0, :] = m.node_type("Wall").value
+    fl[:, ny - 1, :] = m.node_type("Wall").value
+    fl[:, 1:4, 0] = m.node_type("WVelocity").value | mrt
+    fl[:, 4, 0] = m.node_type("WVelocity").value | m.node_type("Heater").value | mrt
+    fl[:, 5:ny - 1, 0] = m.node_type("WPressure").value | mrt
+    fl[:, 1:6, nx - 1] = m.node_type("EPressure").value | mrt
+    fl[:, 6:ny - 1, nx - 1] = m.node_type("EVelocity").value | mrt
+    fl[:, 2:4, 4] |= m.node_type("Heater").value
+    fl[:, 5, 7] |= m.node_type("Thermometer").value
+    fl[:, 6, 8] |= m.node_type("Thermometer").value
+    fl[:, 1:ny - 1, 12] |= m.node_type("Outlet").value
+    fl[:, 4, 10] = m.node_type("Solid").value | mrt
+    fl[:, 6, 10] = 0
+    lat.set_flags(fl)
+    for k, v in {"nu0": 0.1, "InletVelocity": 0.02, "InletPressure": 0.003, "InletTemperature": 1.1,
+                 "InitTemperature": 1.0, "HeaterTemperature": 1.4, "FluidAlpha": 0.08, "SolidAlpha": 0.03,
+                 "LimitTemperature": 1.05, "FluxInObj": 0.4, "HeatFluxInObj": 1.0, "HeatSquareFluxInObj": -0.3,
+                 "TemperatureInObj": 0.6, "HighTemperatureInObj": 2.0, "LowTemperatureInObj": 0.7}.items():
+        lat.set_setting(k, v)
+    lat.init()
+    f = lat.fields_interior().clone()
+    g = torch.Generator().manual_seed(7)
+    f = f * (1 + 0.02 * torch.rand(f.shape, generator=g, dtype=f.dtype)).to(f.device)
+    wi = m.field_index("w")
+    f[wi] = (0.4 + 0.5 * torch.rand(f[wi].shape, generator=g, dtype=f.dtype)).to(f.device)
+    lat.set_fields_interior(f)
+    ad = Adjoint(lat, reverse=reverse)
+    ad.unsteady(steps)
+    return lat, ad
+
+
+def _check_d2q9_heat(device):
+    lat_r, r = _d2q9_heat_case(device, True)
+    lat_d, d = _d2q9_heat_case(device, False)
+    a, b = r.a0.cpu(), d.a0.cpu()
+    scale = b.abs().max().item()
+    assert scale > 0
+    assert torch.allclose(a, b, rtol=0, atol=1e-12 * scale), (a - b).abs().max().item() / scale
+    assert abs(r.J - d.J) <= 1e-13 * abs(d.J)
+    gw_r, gw_d = r.field_gradient("w"), d.field_gradient("w")
+    assert np.abs(gw_d).max() > 0
+    np.testing.assert_allclose(gw_r, gw_d, rtol=0, atol=1e-12 * np.abs(gw_d).max())
+
+
+def test_d2q9_heat_adj_reverse_sweep_matches_dual_cpu():
+    _check_d2q9_heat("cpu")
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not torch.cuda.is_available(), reason="no GPU")
+def test_d2q9_heat_adj_reverse_sweep_matches_dual_gpu():
+    _check_d2q9_heat("cuda")
