@@ -32,6 +32,15 @@ adjoint)
   step "gpu adjoint tests" 600 $O/pytest_gpu_adjoint.log python -u -m pytest tests/test_gpu_adjoint.py -v -m gpu --timeout 300 --timeout-method thread
   step "adjoint bench 64" 300 $O/bench_adjoint_64.json python tools/bench_adjoint.py --size 64 --steps 40
   step "adjoint bench 128" 400 $O/bench_adjoint_128.json python tools/bench_adjoint.py --size 128 --steps 80 ;;
+adbench)
+  for M in d3q19_adj d3q19_heat_adj d3q19_heat_adj_art; do
+    step "adjoint bench $M 128" 300 $O/adbench_${M}_128.json python tools/bench_adjoint.py --model $M --size 128 --steps 20
+  done
+  step "adjoint bench d3q19_heat_adj 128 dual" 300 $O/adbench_d3q19_heat_adj_128_dual.json python tools/bench_adjoint.py --model d3q19_heat_adj --size 128 --steps 20 --dual
+  for M in d2q9_adj d2q9_heat_adj; do
+    step "adjoint bench $M 2048^2" 300 $O/adbench_${M}_2048.json python tools/bench_adjoint.py --model $M --size 2048 --steps 20
+  done
+  step "adjoint bench d2q9_adj 2048^2 dual" 300 $O/adbench_d2q9_adj_2048_dual.json python tools/bench_adjoint.py --model d2q9_adj --size 2048 --steps 20 --dual ;;
 addiag)
   for V in "" row row_o1 row_w1; do
     step "adjoint diag ${V:-flat}" 300 $O/adjoint_diag_${V:-flat}.jsonl env TCLB_AD_VARIANT=$V TCLB_NO_BUILD=1 python tools/adjoint_diag.py --repeats 2

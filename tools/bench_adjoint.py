@@ -1,9 +1,10 @@
 #!/usr/bin/env python3
-"""Timing of the unsteady adjoint (d3q19_adj porous duct) on the GPU adjoint executor:
-primal steps/s, adjoint steps/s (each reverse step = checkpoint recompute + dual-number
-sweep with the device adjoint push), and the gradient norm.
+"""Timing of the unsteady adjoint of the ADJOINT models on the GPU adjoint executor:
+primal steps/s, adjoint steps/s (each reverse step = checkpoint recompute + the node
+adjoints: hand-written reverse sweeps where the model has them, Model.set_reverse, else
+dual-number passes — --dual forces those everywhere), and the gradient norm.
 
-    python tools/bench_adjoint.py --size 128 --steps 20
+    python tools/bench_adjoint.py --model d3q19_heat_adj --size 128 --steps 20
 """
 import argparse
 import json
@@ -17,52 +18,102 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--size", type=int, default=128)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--device", default="cuda")
-    a = ap.parse_args()
-    from tclb_amd.adjoint import Adjoint
+def setup(model: str, n: int, dev):
+    """a design-optimisation case of the model on an n^3 (3-D) or n^2 (2-D) lattice: inlet /
+    outlet planes in x, a design block, objectives on; returns the lattice"""
     from tclb_amd.lattice import Lattice
-    n = a.size
-    dev = torch.device(a.device)
-    lat = Lattice("d3q19_adj", (n, n, n), device=dev)
+    from tclb_amd.models import registry
+    m = registry.get(model)
+    shape = (n, n, n) if m.dims == 3 else (n, n, 1)
+    lat = Lattice(model, shape, device=dev)
     m = lat.model
-    mrt = m.node_type("MRT").value
+    nt = lambda name: m.node_type(name).value  # noqa: E731
+    mrt = nt("MRT")
     fl = np.full((lat.NZ, lat.NY, n), mrt, dtype=np.uint32)
-    fl[:, :, 0] = m.node_type("WPressure").value | mrt
-    fl[:, :, n - 1] = m.node_type("EPressure").value | mrt
-    fl[:, :, n // 4 + 4] |= m.node_type("Outlet").value
-    fl[:, :, 2:n // 4] |= m.node_type("DesignSpace").value
+    settings = {}
+    if model == "d3q19_adj":
+        fl[:, :, 0] = nt("WPressure") | mrt
+        fl[:, :, n - 1] = nt("EPressure") | mrt
+        fl[:, :, n // 4 + 4] |= nt("Outlet")
+        settings = {"nu": 0.1, "InletDensity": 1.01, "FluxInObj": 1.0, "Theta": 1.0}
+    elif model in ("d3q19_heat_adj", "d3q19_heat_adj_art"):
+        fl[:, 0, :] = nt("Wall")
+        fl[:, n - 1, :] = nt("Wall")
+        fl[:, 1:n // 8, n // 8] |= nt("Heater")
+        fl[:, :, n // 4 + 4] |= nt("Outlet")
+        if model == "d3q19_heat_adj_art":
+            fl[:, 1:n - 1, 0] = nt("WVelocity") | mrt
+        settings = {"nu": 0.1, "FluidAlpha": 0.05, "Velocity": 0.01, "Temperature": 1.2, "HeatFluxInObj": 1.0,
+                    "FluxInObj": 0.2}
+        if model == "d3q19_heat_adj_art":
+            settings["SolidAlpha"] = 0.02
+    elif model in ("d2q9_adj", "d2q9_heat_adj"):
+        fl[:, 0, :] = nt("Wall")
+        fl[:, n - 1, :] = nt("Wall")
+        fl[:, 1:n - 1, 0] = nt("WVelocity") | mrt
+        fl[:, 1:n - 1, n - 1] = nt("EPressure") | mrt
+        fl[:, 1:n - 1, n // 4 + 4] |= nt("Outlet")
+        if model == "d2q9_adj":
+            settings = {"nu": 0.1, "Velocity": 0.01, "OutletFluxInObj": 1.0, "PressureLossInObj": 0.5}
+        else:
+            settings = {"nu0": 0.1, "InletVelocity": 0.01, "FluidAlpha": 0.05, "SolidAlpha": 0.02,
+                        "HeatFluxInObj": 1.0}
+    else:
+        raise SystemExit(f"no adjoint bench case for {model}")
+    if m.node_type("DesignSpace") is not None:
+        if m.dims == 3:
+            fl[:, 1:n - 1, 2:n // 4] |= nt("DesignSpace")
+        else:
+            fl[:, 1:n - 1, 2:n // 4] |= nt("DesignSpace")
     lat.set_flags(fl.astype(np.uint16 if m.flag_bits == 16 else np.uint32))
-    for k, v in {"nu": 0.1, "InletDensity": 1.01, "FluxInObj": 1.0, "Theta": 1.0}.items():
+    for k, v in settings.items():
         lat.set_setting(k, v)
     lat.init()
     wi = m.field_index("w")
     f = lat.fields_interior().clone()
     f[wi, :, :, 2:n // 4] = 0.7
     lat.set_fields_interior(f)
+    return lat
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--model", default="d3q19_adj")
+    ap.add_argument("--size", type=int, default=128, help="n (n^3 for 3-D models, n^2 for 2-D)")
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--device", default="cuda")
+    ap.add_argument("--dual", action="store_true", help="dual-number passes everywhere (no reverse sweeps)")
+    a = ap.parse_args()
+    from tclb_amd.adjoint import Adjoint
+    n = a.size
+    dev = torch.device(a.device)
+    lat = setup(a.model, n, dev)
     sync = torch.cuda.synchronize if dev.type == "cuda" else (lambda: None)
+    lat.iterate(2)
     sync()
     t0 = time.perf_counter()
     lat.iterate(a.steps)
     sync()
     tp = time.perf_counter() - t0
-    ad = Adjoint(lat)
+    ad = Adjoint(lat, reverse=not a.dual)
     sync()
     t0 = time.perf_counter()
     ad.unsteady(a.steps)
     sync()
     ta = time.perf_counter() - t0
     g = ad.field_gradient("w")
-    nodes = n ** 3
-    print(json.dumps({"case": f"d3q19_adj unsteady adjoint {n}^3", "device": a.device, "steps": a.steps,
+    nodes = lat.nodes
+    ok = bool(np.isfinite(ad.J) and np.all(np.isfinite(g)))
+    print(json.dumps({"case": f"{a.model} unsteady adjoint {'x'.join(map(str, lat.gshape))}", "device": a.device,
+                      "steps": a.steps, "reverse_sweeps": bool(ad.reverse),
                       "primal_ms_per_step": round(tp / a.steps * 1e3, 3),
                       "adjoint_ms_per_step": round(ta / a.steps * 1e3, 3),
+                      "adjoint_over_primal": round(ta / tp, 2),
                       "adjoint_MLUPS": round(nodes * a.steps / ta / 1e6, 2),
-                      "J": ad.J, "grad_w_absmax": float(np.abs(g).max()),
+                      "J": ad.J, "grad_w_absmax": float(np.abs(g).max()), "finite": ok,
                       "tangent_budget": ad.lib.tangents}), flush=True)
+    if not ok:
+        sys.exit(3)
 
 
 if __name__ == "__main__":
