@@ -31,4 +31,5 @@ def build() -> Model:
     m.add_node_type("Obj1", "OBJECTIVE")
     m.add_node_type("Obj2", "OBJECTIVE")
     m.set_dynamics("experimental/d2q9_diff.inc")
+    m.set_reverse("Run", "rev_ok_run", "rev_run")
     return m

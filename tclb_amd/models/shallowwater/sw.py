@@ -39,4 +39,5 @@ def build() -> Model:
     m.add_node_type("BGK", "COLLISION")
     m.add_node_type("MRT", "COLLISION")
     m.set_dynamics("shallowwater/sw.inc")
+    m.set_reverse("Run", "rev_ok_run", "rev_run")
     return m

@@ -330,3 +330,100 @@ def test_d2q9_heat_adj_reverse_sweep_matches_dual_cpu():
 @pytest.mark.skipif(not torch.cuda.is_available(), reason="no GPU")
 def test_d2q9_heat_adj_reverse_sweep_matches_dual_gpu():
     _check_d2q9_heat("cuda")
+
+
+# ---------------------------------------------------------------- sw (shallow water)
+def _sw_case(device, reverse, steps=10):
+    nx, ny = 16, 10
+    lat = Lattice("sw", (nx, ny, 1), device=torch.device(device))
+    m = lat.model
+    mrt = m.node_type("MRT").value
+    fl = np.full((lat.NZ, lat.NY, nx), mrt, dtype=np.uint32)
+    fl[:, 0, :] = m.node_type("Wall").value
+    fl[:, ny - 1, :] = m.node_type("Wall").value
+    fl[:, 1:5, 0] = m.node_type("WVelocity").value | mrt
+    fl[:, 5:ny - 1, 0] = m.node_type("WPressure").value | mrt
+    fl[:, 1:6, nx - 1] = m.node_type("EPressure").value | mrt
+    fl[:, 6:ny - 1, nx - 1] = m.node_type("EVelocity").value | mrt
+    fl[:, 2:7, 5:9] |= m.node_type("Obj1").value
+    fl[:, 4, 10] = m.node_type("BGK").value
+    fl[:, 6, 10] = 0
+    lat.set_flags(fl)
+    for k, v in {"nu": 0.1, "InletVelocity": 0.01, "Gravity": 0.2, "Height": 1.0, "EnergySink": 0.1,
+                 "TotalDiffInObj": 0.5, "EnergyGainInObj": 1.0, "MaterialInObj": 0.05}.items():
+        lat.set_setting(k, v)
+    lat.init()
+    f = lat.fields_interior().clone()
+    g = torch.Generator().manual_seed(8)
+    f = f * (1 + 0.02 * torch.rand(f.shape, generator=g, dtype=f.dtype)).to(f.device)
+    wi = m.field_index("w")
+    f[wi] = (0.4 + 0.5 * torch.rand(f[wi].shape, generator=g, dtype=f.dtype)).to(f.device)
+    lat.set_fields_interior(f)
+    ad = Adjoint(lat, reverse=reverse)
+    ad.unsteady(steps)
+    return lat, ad
+
+
+def _check_generic(case, device):
+    lat_r, r = case(device, True)
+    lat_d, d = case(device, False)
+    assert r.reverse and not d.reverse
+    a, b = r.a0.cpu(), d.a0.cpu()
+    scale = b.abs().max().item()
+    assert scale > 0
+    assert torch.allclose(a, b, rtol=0, atol=1e-12 * scale), (a - b).abs().max().item() / scale
+    assert abs(r.J - d.J) <= 1e-13 * abs(d.J)
+    gw_r, gw_d = r.field_gradient("w"), d.field_gradient("w")
+    assert np.abs(gw_d).max() > 0
+    np.testing.assert_allclose(gw_r, gw_d, rtol=0, atol=1e-12 * np.abs(gw_d).max())
+
+
+def test_sw_reverse_sweep_matches_dual_cpu():
+    _check_generic(_sw_case, "cpu")
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not torch.cuda.is_available(), reason="no GPU")
+def test_sw_reverse_sweep_matches_dual_gpu():
+    _check_generic(_sw_case, "cuda")
+
+
+# ---------------------------------------------------------------- d2q9_diff
+def _diff_case(device, reverse, steps=10):
+    nx, ny = 16, 10
+    lat = Lattice("d2q9_diff", (nx, ny, 1), device=torch.device(device))
+    m = lat.model
+    mrt = m.node_type("MRT").value
+    fl = np.full((lat.NZ, lat.NY, nx), mrt, dtype=np.uint32)
+    fl[:, 0, :] = m.node_type("Wall").value
+    fl[:, ny - 1, :] = m.node_type("Wall").value
+    fl[:, 1:ny - 1, 0] = m.node_type("WPressure").value | mrt
+    fl[:, 1:ny - 1, nx - 1] = m.node_type("EPressure").value | mrt
+    fl[:, 2:5, 5:9] |= m.node_type("Obj1").value
+    fl[:, 6:8, 5:9] |= m.node_type("Obj2").value
+    fl[:, 5, 10] = 0
+    lat.set_flags(fl)
+    for k, v in {"nu0": 0.05, "nu1": 0.2, "InitDensity": 1.0, "InletDensity": 1.02, "OutletDensity": 0.99,
+                 "DiffInObj": 1.0}.items():
+        lat.set_setting(k, v)
+    lat.init()
+    f = lat.fields_interior().clone()
+    g = torch.Generator().manual_seed(9)
+    f = f * (1 + 0.02 * torch.rand(f.shape, generator=g, dtype=f.dtype)).to(f.device)
+    wi, ri = m.field_index("w"), m.field_index("r")
+    f[wi] = (0.2 + 0.6 * torch.rand(f[wi].shape, generator=g, dtype=f.dtype)).to(f.device)
+    f[ri] = (0.9 + 0.2 * torch.rand(f[ri].shape, generator=g, dtype=f.dtype)).to(f.device)
+    lat.set_fields_interior(f)
+    ad = Adjoint(lat, reverse=reverse)
+    ad.unsteady(steps)
+    return lat, ad
+
+
+def test_d2q9_diff_reverse_sweep_matches_dual_cpu():
+    _check_generic(_diff_case, "cpu")
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not torch.cuda.is_available(), reason="no GPU")
+def test_d2q9_diff_reverse_sweep_matches_dual_gpu():
+    _check_generic(_diff_case, "cuda")
