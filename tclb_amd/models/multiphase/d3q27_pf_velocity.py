@@ -143,7 +143,7 @@ def build(q27: bool = False, bgk: bool = False, thermo: bool = False, planarbenc
         load_iteration += ["Thermal"]
     m.add_stage("PhaseInit", "Init", save_fields=save_initial_PF)
     m.add_stage("BaseInit", "Init_distributions", save_fields=save_initial)
-    m.add_stage("calcPhase", "calcPhaseF", save_fields=["PhaseF"], load_densities=load_phase)
+    m.add_stage("calcPhase", "calcPhaseF", save_fields=["PhaseF"], load_densities=load_phase, lazy_load=True)
     # the collision's phase-field gradient and normal read PhaseF through its 27-point (or
     # 125-point, geometric) stencil: staged in an LDS tile on the GPU (k_tile)
     m.add_stage("BaseIter", "Run", save_fields=save_iteration, load_densities=load_iteration, lds=["PhaseF"])
