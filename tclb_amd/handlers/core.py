@@ -956,6 +956,35 @@ class RemoteForceInterface(Action):
         units = {"m": u.alt("1m"), "s": u.alt("1s"), "kg": u.alt("1kg")}
         rp = RemoteParticles(self.node.get("address", "127.0.0.1:0"), comm=lat.comm, units=units,
                              box=list(lat.gshape), timeout=float(self.node.get("timeout", "120")))
+        # negotiated variables and statistics (reference acRemoteForceInterface.cpp:26-82):
+        # "output", the element's single child as "content", every other attribute as a
+        # number in lattice units
+        rp.set_var("output", s.outpath)
+        kids = list(self.node)
+        if len(kids) > 1:
+            raise ValueError("only a single element/CDATA allowed inside <RemoteForceInterface>")
+        content = None
+        if kids:
+            import xml.etree.ElementTree as ET
+            content = ET.tostring(kids[0], encoding="unicode").strip()
+        elif (self.node.text or "").strip():
+            content = self.node.text.strip()
+        if content is not None:
+            rp.set_var("content", content)
+        stats, prefix, every = False, s.outpath + "_RFI", 200
+        own = ("integrator", "address", "spawn", "timeout", "use_box", "omega", "torque")
+        for k, v in self.node.attrib.items():
+            if k == "stats":
+                stats = v.lower() in ("1", "true", "yes", "y")
+            elif k == "stats_iter":
+                every, stats = int(round(u.alt(v))), True
+            elif k == "stats_prefix":
+                prefix, stats = v, True
+            elif k not in own:
+                rp.set_var(k, "%.15g" % u.alt(v))
+        if stats:
+            log.output(f"Asking for stats on RFI ({prefix} every {every} it)")
+            rp.enable_stats(prefix, every)
         proc = None
         cmd = self.node.get("spawn")
         if cmd and lat.comm.rank == 0:

@@ -117,3 +117,54 @@ def test_empty_integrator(tmp_path):
     s = Solver("auto_d3q19_part", root, conffile=str(tmp_path / "case.xml"), device="cpu")
     s.run()
     assert s.iter == 6 and s.particles.n == 0
+
+
+def test_vars_and_stats_negotiated(tmp_path):
+    """reference Negotiate: named variables travel both ways (the peer's value wins a
+    clash), statistics are collected when either side asks; the calculator and the
+    integrator each append a line of mean particle counts and phase times every `iter`
+    exchanges (reference enableStats / printStats)"""
+    rp = RemoteParticles("127.0.0.1:0")
+    rp.set_var("output", str(tmp_path / "run"))
+    rp.set_var("content", json.dumps({"particles": [PART]}))
+    rp.set_var("shared", "calc")
+    rp.enable_stats(str(tmp_path / "rfi"), 2)
+    got = {}
+
+    def integrator():
+        c = IntegratorClient(rp.address, vars={"code": "test", "shared": "integ"})
+        got["vars"] = dict(c.vars)
+        got["stats"] = c.stats is not None
+        x = np.array([PART["x"]])
+        for _ in range(5):
+            if c.exchange(x, np.zeros((1, 3)), np.zeros((1, 3)), np.array([PART["r"]])) is None:
+                break
+        c.close()
+    t = threading.Thread(target=integrator)
+    t.start()
+    lat = _lat()
+    rp.accept()
+    assert rp.vars["code"] == "test" and rp.vars["shared"] == "integ" and rp.vars["output"].endswith("run")
+    lat.particles = rp
+    lat.init()
+    lat.iterate(4)
+    rp.close()
+    t.join(20)
+    assert got["vars"]["content"] and got["vars"]["shared"] == "calc" and got["stats"]
+    calc = (tmp_path / "rfi_calculator_P00.txt").read_text().splitlines()
+    integ = (tmp_path / "rfi_integrator_P00.txt").read_text().splitlines()
+    assert calc[0].startswith("size_iter, size_000, dt_wait_particles")
+    assert len(calc) >= 3 and calc[1].split(", ")[0] == "2" and float(calc[1].split(", ")[1]) == 1.0
+    assert integ[0].startswith("size_iter, size_000, dt_integrate") and len(integ) >= 2
+
+
+def test_handler_sends_content_output_and_attributes(tmp_path):
+    """<RemoteForceInterface> passes "output", its child as "content" and its other
+    attributes as numbers (reference acRemoteForceInterface.cpp:26-82); the stand-alone
+    simplepart takes its particles from "content" when no --config is given"""
+    from tclb_amd.particles.rfi import negotiate
+    mine = {"output": "o", "content": "{}", "Velocity": "0.01"}
+    vars_, st = negotiate(mine, {"enabled": True, "prefix": "", "iter": 0}, {"vars": {"x": "1"},
+                                                                          "stats": {"prefix": "p", "iter": 5}})
+    assert vars_ == {"output": "o", "content": "{}", "Velocity": "0.01", "x": "1"}
+    assert st == {"enabled": True, "prefix": "p", "iter": 5}

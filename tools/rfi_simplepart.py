@@ -42,6 +42,25 @@ def main():
     acc = np.asarray(cfg.get("acc", [0, 0, 0]), float)
     per = np.asarray(cfg.get("periodic", [0, 0, 0]), float)
     client = IntegratorClient(a.address)
+    # the calculator's configuration (reference simplepart.cpp:100-145: "content" holds
+    # the configuration, "output" names the log)
+    if not a.config and client.has_var("content"):
+        try:
+            cfg = json.loads(client.get_var("content"))
+        except ValueError:
+            cfg = {}
+        ps = [] if a.empty else cfg.get("particles", [])
+        n = len(ps)
+        x = np.array([p["x"] for p in ps], float).reshape(n, 3)
+        v = np.array([p.get("v", [0, 0, 0]) for p in ps], float).reshape(n, 3)
+        w = np.array([p.get("omega", [0, 0, 0]) for p in ps], float).reshape(n, 3)
+        r = np.array([p["r"] for p in ps], float)
+        m = np.array([p.get("m") or 4.0 / 3.0 * math.pi * p["r"] ** 3 for p in ps], float)
+        fixed = np.array([bool(p.get("fixed", False)) for p in ps])
+        acc = np.asarray(cfg.get("acc", [0, 0, 0]), float)
+        per = np.asarray(cfg.get("periodic", [0, 0, 0]), float)
+    if a.log is None and client.has_var("output") and n:
+        a.log = client.get_var("output") + "_SP_Log.csv"
     log = open(a.log, "w") if a.log else None
     if log:
         log.write("Iteration," + ",".join(f"p{i}_{c}{d}" for i in range(n) for c in ("", "v", "f") for d in "xyz") + "\n")
