@@ -144,9 +144,9 @@ def build(q27: bool = False, bgk: bool = False, thermo: bool = False, planarbenc
     m.add_stage("PhaseInit", "Init", save_fields=save_initial_PF)
     m.add_stage("BaseInit", "Init_distributions", save_fields=save_initial)
     m.add_stage("calcPhase", "calcPhaseF", save_fields=["PhaseF"], load_densities=load_phase, lazy_load=True)
-    # the collision's phase-field gradient and normal read PhaseF through its 27-point (or
-    # 125-point, geometric) stencil: staged in an LDS tile on the GPU (k_tile)
-    m.add_stage("BaseIter", "Run", save_fields=save_iteration, load_densities=load_iteration, lds=["PhaseF"])
+    # (the collision's PhaseF stencil stays on global loads: an LDS tile of it made the
+    # latency-bound collision 7-10 % slower, profiles/README.md r04a)
+    m.add_stage("BaseIter", "Run", save_fields=save_iteration, load_densities=load_iteration)
     m.add_stage("InitFromFieldsStage", "InitFromFieldsStage", save_fields=save_initial_PF, load_densities=["init"])
     if geometric:           # Dynamics.R:129-135
         m.add_stage("WallInit_CA", "Init_wallNorm", save_fields=["nw", "solid_boundary"] + extra_bc)

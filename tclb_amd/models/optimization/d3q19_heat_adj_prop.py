@@ -65,4 +65,5 @@ def build() -> Model:
     m.add_node_type("Thermometer", "OBJECTIVE")
     m.add_codegen(_blocks)
     m.set_dynamics("optimization/d3q19_heat_adj_prop.inc")
+    m.set_reverse("Run", "rev_ok_run", "rev_run")
     return m

@@ -427,3 +427,53 @@ def test_d2q9_diff_reverse_sweep_matches_dual_cpu():
 @pytest.mark.skipif(not torch.cuda.is_available(), reason="no GPU")
 def test_d2q9_diff_reverse_sweep_matches_dual_gpu():
     _check_generic(_diff_case, "cuda")
+
+
+# ---------------------------------------------------------------- d3q19_heat_adj_prop
+def _prop_case(device, reverse, steps=8):
+    nx, ny, nz = 12, 7, 6
+    lat = Lattice("d3q19_heat_adj_prop", (nx, ny, nz), device=torch.device(device))
+    m = lat.model
+    mrt = m.node_type("MRT").value
+    fl = np.full((lat.NZ, lat.NY, nx), mrt, dtype=np.uint32)
+    fl[:, 0, :] = m.node_type("Wall").value
+    fl[:, ny - 1, :] = m.node_type("Wall").value
+    fl[:, 1:4, 0] = m.node_type("WVelocity").value | mrt
+    fl[:, 4:ny - 1, 0] = m.node_type("WPressure").value | mrt
+    fl[:, 3, 0] = m.node_type("WPressureL").value | mrt
+    fl[:, 1:ny - 1, nx - 1] = m.node_type("EPressure").value | mrt
+    fl[:, 1:3, 3] |= m.node_type("Heater").value
+    fl[:, 4:6, 3] |= m.node_type("HeatSource").value
+    fl[:, 3, 6] |= m.node_type("Thermometer").value
+    fl[:, 1:ny - 1, 9] |= m.node_type("Outlet").value
+    fl[:, 2:5, 4:8] |= m.node_type("DesignSpace").value
+    fl[:, 2:5, 5:8] |= m.node_type("Propagate").value
+    fl[1, 3, 10] = m.node_type("BGK").value
+    fl[2, 3, 10] = 0
+    lat.set_flags(fl)
+    for k, v in {"nu": 0.1, "FluidAlpha": 0.08, "SolidAlpha": 0.02, "InletVelocity": 0.02, "InletPressure": 0.003,
+                 "InletTemperature": 1.1, "HeaterTemperature": 1.3, "HeatSource": 0.01, "LimitTemperature": 1.05,
+                 "PropagateX": 0.3, "FluxInObj": 0.4, "HeatFluxInObj": 1.0, "HeatSquareFluxInObj": -0.3,
+                 "TemperatureInObj": 0.6, "HighTemperatureInObj": 2.0, "LowTemperatureInObj": 0.7,
+                 "MaterialPenaltyInObj": 0.05}.items():
+        lat.set_setting(k, v)
+    lat.init()
+    f = lat.fields_interior().clone()
+    g = torch.Generator().manual_seed(10)
+    f = f * (1 + 0.02 * torch.rand(f.shape, generator=g, dtype=f.dtype)).to(f.device)
+    wi = m.field_index("w")
+    f[wi] = (0.4 + 0.5 * torch.rand(f[wi].shape, generator=g, dtype=f.dtype)).to(f.device)
+    lat.set_fields_interior(f)
+    ad = Adjoint(lat, reverse=reverse)
+    ad.unsteady(steps)
+    return lat, ad
+
+
+def test_prop_reverse_sweep_matches_dual_cpu():
+    _check_generic(_prop_case, "cpu")
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not torch.cuda.is_available(), reason="no GPU")
+def test_prop_reverse_sweep_matches_dual_gpu():
+    _check_generic(_prop_case, "cuda")
