@@ -41,6 +41,23 @@ adbench)
     step "adjoint bench $M 2048^2" 300 $O/adbench_${M}_2048.json python tools/bench_adjoint.py --model $M --size 2048 --steps 20
   done
   step "adjoint bench d2q9_adj 2048^2 dual" 300 $O/adbench_d2q9_adj_2048_dual.json python tools/bench_adjoint.py --model d2q9_adj --size 2048 --steps 20 --dual ;;
+adbench80)
+  for M in d3q19_adj d3q19_heat_adj d3q19_heat_adj_art d3q19_heat_adj_prop; do
+    step "adjoint bench $M 128 x80" 400 $O/adbench80_${M}_128.json python tools/bench_adjoint.py --model $M --size 128 --steps 80
+  done
+  for M in d2q9_adj d2q9_heat_adj; do
+    step "adjoint bench $M 2048^2 x80" 400 $O/adbench80_${M}_2048.json python tools/bench_adjoint.py --model $M --size 2048 --steps 80
+  done
+  step "rocprof adjoint d3q19_heat_adj" 400 $O/prof_adj_heat.log rocprofv3 --kernel-trace --stats -d $O/prof_adj_heat -o run --output-format csv -- python3 $R/tools/bench_adjoint.py --model d3q19_heat_adj --size 128 --steps 40 ;;
+tiles2)
+  step "pf 384 fp64" 600 $O/tiles2_pf384_fp64.jsonl python tools/perf_models.py --models d3q27_pf_velocity --n3 384 --steps 20 --rounds 2 --allow-invalid
+  step "pf 384 mixed-shift" 600 $O/tiles2_pf384_ms.jsonl python tools/perf_models.py --models d3q27_pf_velocity --n3 384 --steps 20 --precision mixed-shift --rounds 2 --allow-invalid
+  step "rocprof pf384 ms" 400 $O/prof_pf384_ms.log rocprofv3 --kernel-trace --stats -d $O/prof_pf384_ms -o run --output-format csv -- python3 $R/tools/perf_models.py --models d3q27_pf_velocity --n3 384 --steps 10 --precision mixed-shift ;;
+configs4)
+  step "configs fp64 100 steps" 600 $O/configs_fp64_100.jsonl python tools/bench_configs.py --steps 100 --warmup 10
+  step "configs mixed-shift 100 steps" 600 $O/configs_ms_100.jsonl python tools/bench_configs.py --steps 100 --warmup 10 --precision mixed-shift
+  step "part256 1000 steps" 600 $O/part256_1000.jsonl python tools/bench_configs.py --configs part256 --steps 1000 --warmup 10
+  step "rocprof part256" 400 $O/prof_part256.log rocprofv3 --kernel-trace --stats -d $O/prof_part256 -o run --output-format csv -- python3 $R/tools/bench_configs.py --configs part256 --steps 50 --warmup 5 ;;
 addiag)
   for V in "" row row_o1 row_w1; do
     step "adjoint diag ${V:-flat}" 300 $O/adjoint_diag_${V:-flat}.jsonl env TCLB_AD_VARIANT=$V TCLB_NO_BUILD=1 python tools/adjoint_diag.py --repeats 2

@@ -47,6 +47,16 @@ def setup(model: str, n: int, dev):
                     "FluxInObj": 0.2}
         if model == "d3q19_heat_adj_art":
             settings["SolidAlpha"] = 0.02
+    elif model == "d3q19_heat_adj_prop":
+        fl[:, 0, :] = nt("Wall")
+        fl[:, n - 1, :] = nt("Wall")
+        fl[:, 1:n - 1, 0] = nt("WVelocity") | mrt
+        fl[:, 1:n // 8, n // 8] |= nt("Heater")
+        fl[:, :, n // 4 + 4] |= nt("Outlet")
+        fl[:, 1:n - 1, 3:n // 4] |= nt("Propagate")
+        settings = {"nu": 0.1, "FluidAlpha": 0.05, "SolidAlpha": 0.02, "InletVelocity": 0.01,
+                    "InletTemperature": 1.0, "HeaterTemperature": 1.2, "PropagateX": 0.2, "HeatFluxInObj": 1.0,
+                    "FluxInObj": 0.2}
     elif model in ("d2q9_adj", "d2q9_heat_adj"):
         fl[:, 0, :] = nt("Wall")
         fl[:, n - 1, :] = nt("Wall")
