@@ -151,7 +151,7 @@ def build(q27: bool = False, bgk: bool = False, thermo: bool = False, planarbenc
     if geometric:           # Dynamics.R:129-135
         m.add_stage("WallInit_CA", "Init_wallNorm", save_fields=["nw", "solid_boundary"] + extra_bc)
         m.add_stage("calcWall_CA", "calcWallPhase", save_fields=["PhaseF"],
-                    load_densities=["nw", "gradPhi", "PF", "solid_boundary"] + extra_bc)
+                    load_densities=["nw", "gradPhi", "PF", "solid_boundary"] + extra_bc, lazy_load=True)
         m.add_stage("calcPhaseGrad", "calcPhaseGrad", save_fields=["gradPhi"],
                     load_densities=["nw", "PF", "solid_boundary"])
         m.add_stage("calcPhaseGrad_init", "calcPhaseGrad_init", save_fields=["gradPhi"],
@@ -159,9 +159,9 @@ def build(q27: bool = False, bgk: bool = False, thermo: bool = False, planarbenc
     else:
         m.add_stage("WallInit", "Init_wallNorm", save_fields=["nw", "solid_boundary"] + extra_bc)
         m.add_stage("calcWall", "calcWallPhase", save_fields=["PhaseF"],
-                    load_densities=["nw", "solid_boundary"] + extra_bc)
+                    load_densities=["nw", "solid_boundary"] + extra_bc, lazy_load=True)
     m.add_stage("calcWallPhase_correction", "calcWallPhase_correction", save_fields=["PhaseF"],
-                load_densities=["nw", "solid_boundary"])
+                load_densities=["nw", "solid_boundary"], lazy_load=True)
     if thermo:
         # Dynamics.R:124-134, 142-147 (explicit RK4 of the energy equation)
         T3 = ["Temp", "Cond", "SurfaceTension"]

@@ -1,0 +1,61 @@
+"""Production-size checks on the GPU (round-3 verdict: the GPU tests ran at toy sizes
+only).  The headline case — d3q27 MRT channel 512^3, fp64: 58 GB of snapshots, field
+offsets past 2^31 bytes — is invariant in x and z (uniform init, walls only in y), so
+after 20 steps the first and last z planes and x columns must be bitwise equal, and the
+total mass must be conserved; the same for the fp32-storage (mixed-shift) layout and for
+the native multi-rank loop (RCCL send/receive to itself) on the 8-GPU slab shape."""
+import os
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+gpu = pytest.mark.gpu
+needs = pytest.mark.skipif(not torch.cuda.is_available(), reason="no GPU")
+
+
+def _channel(shape, precision, comm=None):
+    import bench
+    from tclb_amd.lattice import Lattice
+    from tclb_amd.parallel.comm import LoopbackComm
+    lat = Lattice("d3q27", shape, device=torch.device("cuda", 0), precision=precision,
+                  comm=comm or LoopbackComm())
+    lat.set_flags(bench.channel_flags(lat))
+    lat.set_setting("nu", 0.02)
+    lat.set_setting("ForceX", 1e-6)
+    lat.init()
+    m0 = bench.total_mass(lat, lat.comm)
+    lat.iterate(20)
+    torch.cuda.synchronize()
+    return lat, bench.physics_checks(lat, lat.comm, m0, precision)
+
+
+@gpu
+@needs
+@pytest.mark.parametrize("precision", ["double", "mixed-shift"])
+def test_headline_512_invariants(precision):
+    lat, chk = _channel((512, 512, 512), precision)
+    assert lat.fs * lat.snaps[0].element_size() * lat.nf > 2 ** 31
+    assert chk["z_invariant"] and chk["x_invariant"], chk
+    assert chk["mass_ok"] and chk["globals_finite"], chk
+    # the flow is developing: a y profile exists (walls at y = 0, ny - 1)
+    u = lat.quantity("U")[0, 256, :, 256]
+    assert float(u[256]) > 0.0 and float(u[1]) < float(u[256])
+    del lat
+    torch.cuda.empty_cache()
+
+
+@gpu
+@needs
+def test_native_dist_rccl_slab_invariants(monkeypatch):
+    """the 8-GPU per-rank slab (512x512x64) through the native multi-rank loop with the
+    RCCL transport sending to this rank itself"""
+    from tclb_amd.parallel.comm import LoopbackComm
+    monkeypatch.setenv("TCLB_DIST_TRANSPORT", "rccl")
+    lat, chk = _channel((512, 512, 64), "double", comm=LoopbackComm(exercise_dist_path=True))
+    assert lat._dist is not None and lat._dist.transport == "rccl"
+    assert chk["z_invariant"] and chk["x_invariant"] and chk["mass_ok"], chk
