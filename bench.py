@@ -168,6 +168,12 @@ def main():
 
     lat.iterate(a.warmup, glob_last=False)
     sync()
+    # host cost of a step on an idle queue: the enqueue time of a few steps (launches,
+    # events, RCCL group calls) before the GPU has caught up — outside the timed window
+    th = time.perf_counter()
+    lat.iterate(4, glob_last=False)
+    t_enqueue = (time.perf_counter() - th) / 4
+    sync()
     t0 = time.perf_counter()
     if a.glob_every_step:
         for _ in range(a.steps):
@@ -212,6 +218,7 @@ def main():
             "globals_finite": chk["globals_finite"],
             "checks": chk,
             "host_ms_per_step": round(t_host / max(1, a.steps - 1) * 1e3, 4) if not a.glob_every_step else None,
+            "host_enqueue_ms_per_step": round(t_enqueue * 1e3, 4),
             "loop": ("native-dist/" + lat._dist.transport) if lat._dist is not None else
                     ("native" if lat._native_ok("Iteration") else "python"),
             "baseline_note": "reference publishes no MLUPS (BASELINE.md); vs_baseline null",
