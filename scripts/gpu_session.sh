@@ -49,6 +49,13 @@ adbench80)
     step "adjoint bench $M 2048^2 x80" 400 $O/adbench80_${M}_2048.json python tools/bench_adjoint.py --model $M --size 2048 --steps 80
   done
   step "rocprof adjoint d3q19_heat_adj" 400 $O/prof_adj_heat.log rocprofv3 --kernel-trace --stats -d $O/prof_adj_heat -o run --output-format csv -- python3 $R/tools/bench_adjoint.py --model d3q19_heat_adj --size 128 --steps 40 ;;
+adbench2d)
+  for M in d2q9_kuper_adj d2q9_optimalMixing d2q9_plate; do
+    step "adjoint bench $M 2048^2 x40" 400 $O/adbench_${M}_2048.json python tools/bench_adjoint.py --model $M --size 2048 --steps 40
+  done ;;
+tepsm)
+  step "tePSM 256 fp64 default vs sw2" 600 $O/tepsm_256_ab.jsonl python tools/perf_models.py --models d3q27_tePSM_per_NEBB --n3 256 --steps 20 --rounds 2 --variants ,sw2 --allow-invalid
+  step "rocprof tePSM 256" 400 $O/prof_tepsm.log rocprofv3 --kernel-trace --stats -d $O/prof_tepsm -o run --output-format csv -- python3 $R/tools/perf_models.py --models d3q27_tePSM_per_NEBB --n3 256 --steps 10 ;;
 tiles2)
   step "pf 384 fp64" 600 $O/tiles2_pf384_fp64.jsonl python tools/perf_models.py --models d3q27_pf_velocity --n3 384 --steps 20 --rounds 2 --allow-invalid
   step "pf 384 mixed-shift" 600 $O/tiles2_pf384_ms.jsonl python tools/perf_models.py --models d3q27_pf_velocity --n3 384 --steps 20 --precision mixed-shift --rounds 2 --allow-invalid

@@ -56,4 +56,5 @@ def build() -> Model:
         m.add_node_type(n, "BOUNDARY")
     m.add_node_type("MRT", "COLLISION")
     m.set_dynamics("moving/d2q9_plate.inc")
+    m.set_reverse("Run", "rev_ok_run", "rev_run")
     return m

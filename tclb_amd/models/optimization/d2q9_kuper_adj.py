@@ -65,4 +65,5 @@ def build() -> Model:
         m.add_node_type(n, "OBJECTIVE")
     m.add_node_type("Wet", "ADDITIONALS")
     m.set_dynamics("optimization/d2q9_kuper_adj.inc")
+    m.set_reverse("Run", "rev_ok_run", "rev_run")
     return m

@@ -1,16 +1,24 @@
 """d2q9_optimalMixing — D2Q9 BGK flow driven by a moving lid plus a D2Q5 passive scalar
 (temperature) for mixing optimisation: objective pieces TotalTempSqr/CountCells, wall
-force and power on the moving lid.  Adjoint quantities RhoB/TB come from the generic AD
-adjoint.  Reference: models/optimization/d2q9_optimalMixing/{Dynamics.R, Dynamics.c.Rt}."""
+force and power on the moving lid.  Adjoint quantities RhoB/TB from the reverse sweep
+(Model.set_reverse: rev_run in the .inc, with the emitted equilibria's VJPs).
+Reference: models/optimization/d2q9_optimalMixing/{Dynamics.R, Dynamics.c.Rt}."""
+import numpy as np
+
 from ..dsl import Model
-from ...emit.blocks import feq_block
+from ...emit.blocks import feq_block, vjp_function
+from ...emit.symbolic import mrt_eq
 
 U9 = [[0, 0], [1, 0], [0, 1], [-1, 0], [0, -1], [1, 1], [-1, 1], [-1, -1], [1, -1]]
 U5 = [[0, 0], [1, 0], [0, 1], [-1, 0], [0, -1]]
 
 
 def _blocks(_m):
-    return "\n".join([feq_block("feq9", U9), feq_block("feq5", U5)])
+    out = [feq_block("feq9", U9), feq_block("feq5", U5)]
+    for name, U in (("feq9", U9), ("feq5", U5)):     # (d feq / d (rho, J))^T a
+        eq = mrt_eq(np.asarray(U, dtype=int), orthogonal=False, order=2)
+        out.append(vjp_function(f"{name}_T", ["rho"] + [str(j) for j in eq.J], eq.feq))
+    return "\n".join(out)
 
 
 def build() -> Model:
@@ -44,4 +52,5 @@ def build() -> Model:
     m.add_node_type("MRT", "COLLISION")
     m.add_codegen(_blocks)
     m.set_dynamics("optimization/d2q9_optimalmixing.inc")
+    m.set_reverse("Run", "rev_ok_run", "rev_run")
     return m

@@ -364,7 +364,7 @@ def _sw_case(device, reverse, steps=10):
     return lat, ad
 
 
-def _check_generic(case, device):
+def _check_generic(case, device, param="w"):
     lat_r, r = case(device, True)
     lat_d, d = case(device, False)
     assert r.reverse and not d.reverse
@@ -373,7 +373,9 @@ def _check_generic(case, device):
     assert scale > 0
     assert torch.allclose(a, b, rtol=0, atol=1e-12 * scale), (a - b).abs().max().item() / scale
     assert abs(r.J - d.J) <= 1e-13 * abs(d.J)
-    gw_r, gw_d = r.field_gradient("w"), d.field_gradient("w")
+    if param is None:           # a model without a design field: the state adjoint only
+        return
+    gw_r, gw_d = r.field_gradient(param), d.field_gradient(param)
     assert np.abs(gw_d).max() > 0
     np.testing.assert_allclose(gw_r, gw_d, rtol=0, atol=1e-12 * np.abs(gw_d).max())
 
@@ -477,3 +479,133 @@ def test_prop_reverse_sweep_matches_dual_cpu():
 @pytest.mark.skipif(not torch.cuda.is_available(), reason="no GPU")
 def test_prop_reverse_sweep_matches_dual_gpu():
     _check_generic(_prop_case, "cuda")
+
+
+# ---------------------------------------------------------------- d2q9_optimalMixing
+def _mixing_case(device, reverse, steps=10):
+    nx, ny = 14, 10
+    lat = Lattice("d2q9_optimalMixing", (nx, ny, 1), device=torch.device(device))
+    m = lat.model
+    mrt = m.node_type("MRT").value
+    fl = np.full((lat.NZ, lat.NY, nx), mrt, dtype=np.uint32)
+    fl[:, 0, :] = m.node_type("Wall").value
+    fl[:, :, 0] = m.node_type("Wall").value
+    fl[:, :, nx - 1] = m.node_type("Solid").value
+    fl[:, ny - 1, 1:nx - 1] = m.node_type("NMovingWall").value | mrt
+    fl[:, 4, 6] = 0
+    lat.set_flags(fl)
+    for k, v in {"nu": 0.08, "K": 0.05, "MovingWallVelocity": 0.05, "TotalTempSqrInObj": 1.0,
+                 "NMovingWallForceInObj": 0.7, "MovingWallPowerInObj": -2.0}.items():
+        lat.set_setting(k, v)
+    lat.init()
+    f = lat.fields_interior().clone()
+    g = torch.Generator().manual_seed(11)
+    f = f * (1 + 0.02 * torch.rand(f.shape, generator=g, dtype=f.dtype)).to(f.device)
+    for i in range(5):                         # a temperature pattern to mix
+        gi = m.field_index(f"g[{i}]")
+        f[gi] = (0.1 + 0.2 * torch.rand(f[gi].shape, generator=g, dtype=f.dtype)).to(f.device)
+    lat.set_fields_interior(f)
+    ad = Adjoint(lat, reverse=reverse)
+    ad.unsteady(steps)
+    return lat, ad
+
+
+def test_optimalmixing_reverse_sweep_matches_dual_cpu():
+    _check_generic(_mixing_case, "cpu", param=None)
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not torch.cuda.is_available(), reason="no GPU")
+def test_optimalmixing_reverse_sweep_matches_dual_gpu():
+    _check_generic(_mixing_case, "cuda", param=None)
+
+
+# ---------------------------------------------------------------- d2q9_plate
+def _plate_case(device, reverse, steps=10, bf=1.0):
+    nx, ny = 18, 12
+    lat = Lattice("d2q9_plate", (nx, ny, 1), device=torch.device(device))
+    m = lat.model
+    mrt = m.node_type("MRT").value
+    fl = np.full((lat.NZ, lat.NY, nx), mrt, dtype=np.uint32)
+    fl[:, 0, :] = m.node_type("Wall").value
+    fl[:, ny - 1, 1:nx - 1] = m.node_type("NVelocity").value | mrt
+    fl[:, 1:7, 0] = m.node_type("WVelocity").value | mrt
+    fl[:, 7:ny, 0] = m.node_type("WPressure").value | mrt
+    fl[:, 1:ny, nx - 1] = m.node_type("EPressure").value | mrt
+    fl[:, 1, 1:nx - 1] = m.node_type("SPressure").value | mrt
+    fl[:, 5, 12] = m.node_type("Solid").value
+    lat.set_flags(fl)
+    for k, v in {"nu": 0.05, "VelocityX": 0.03, "VelocityY": 0.01, "Smag": 0.3, "PRAD": 2.5, "SM": 2.0,
+                 "BF": bf, "PX": 7.3, "PY": 5.6, "PR": 0.4, "ExternalForceX": 1e-4,
+                 "ForceXInObj": 1.0, "ForceYInObj": -0.5, "MomentInObj": 0.2, "PowerXInObj": 0.3,
+                 "PowerYInObj": 0.4, "PowerRInObj": -0.6, "PowerInObj": 0.8, "VolumeWInObj": 0.05}.items():
+        lat.set_setting(k, v)
+    for k, v in {"PX": 0.02, "PY": -0.01, "PR": 0.03}.items():
+        lat.set_setting_dt(k, v)
+    lat.init()
+    f = lat.fields_interior().clone()
+    g = torch.Generator().manual_seed(12)
+    f = f * (1 + 0.03 * torch.rand(f.shape, generator=g, dtype=f.dtype)).to(f.device)
+    lat.set_fields_interior(f)
+    ad = Adjoint(lat, reverse=reverse)
+    ad.unsteady(steps)
+    return lat, ad
+
+
+def test_plate_reverse_sweep_matches_dual_cpu():
+    _check_generic(_plate_case, "cpu", param=None)
+    _check_generic(lambda dev, rev: _plate_case(dev, rev, bf=0.0), "cpu", param=None)
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not torch.cuda.is_available(), reason="no GPU")
+def test_plate_reverse_sweep_matches_dual_gpu():
+    _check_generic(_plate_case, "cuda", param=None)
+
+
+# ---------------------------------------------------------------- d2q9_kuper_adj
+def _kuper_case(device, reverse, steps=10):
+    nx, ny = 16, 10
+    lat = Lattice("d2q9_kuper_adj", (nx, ny, 1), device=torch.device(device))
+    m = lat.model
+    mrt = m.node_type("MRT").value
+    fl = np.full((lat.NZ, lat.NY, nx), mrt, dtype=np.uint32)
+    fl[:, 0, :] = m.node_type("Wall").value
+    fl[:, 0, 4:8] |= m.node_type("Wet").value
+    fl[:, ny - 1, :] = m.node_type("MovingWall").value
+    fl[:, 1:5, 0] = m.node_type("WVelocity").value | mrt
+    fl[:, 5:ny - 1, 0] = m.node_type("WPressure").value | mrt
+    fl[:, 1:5, nx - 1] = m.node_type("EPressure").value | mrt
+    fl[:, 5:ny - 1, nx - 1] = m.node_type("EVelocity").value | mrt
+    fl[:, 2:5, 5:9] |= m.node_type("Obj1").value
+    fl[:, 6:8, 5:9] |= m.node_type("Obj2").value
+    fl[:, 1, 10:13] |= m.node_type("Obj3").value
+    fl[:, 4, 11] = m.node_type("BGK").value
+    fl[:, 6, 12] = m.node_type("Solid").value
+    lat.set_flags(fl)
+    for k, v in dict(InitDensity=1.0, WallDensity=1.05, WetDensity=1.1, Temperature=0.56, FAcc=1.0, Magic=0.01,
+                     MagicA=-0.152, MagicF=1.0, Wetting=0.7, GravitationX=1e-3, GravitationY=-2e-4, nu=0.1,
+                     InletVelocity=0.01, InletDensity=1.02, OutletDensity=0.99, MovingWallVelocity=0.02,
+                     FluidVelocityXInObj=1.0, Pressure1InObj=0.5, Pressure2InObj=-0.3, Pressure3InObj=0.2,
+                     Density1InObj=0.4, Density2InObj=0.1, Density3InObj=-0.7).items():
+        lat.set_setting(k, v)
+    lat.init()
+    f = lat.fields_interior().clone()
+    g = torch.Generator().manual_seed(13)
+    f = f * (1 + 0.02 * torch.rand(f.shape, generator=g, dtype=f.dtype)).to(f.device)
+    wi = m.field_index("w")
+    f[wi] = (0.4 + 0.5 * torch.rand(f[wi].shape, generator=g, dtype=f.dtype)).to(f.device)
+    lat.set_fields_interior(f)
+    ad = Adjoint(lat, reverse=reverse)
+    ad.unsteady(steps)
+    return lat, ad
+
+
+def test_kuper_adj_reverse_sweep_matches_dual_cpu():
+    _check_generic(_kuper_case, "cpu")
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not torch.cuda.is_available(), reason="no GPU")
+def test_kuper_adj_reverse_sweep_matches_dual_gpu():
+    _check_generic(_kuper_case, "cuda")

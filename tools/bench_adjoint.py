@@ -68,6 +68,27 @@ def setup(model: str, n: int, dev):
         else:
             settings = {"nu0": 0.1, "InletVelocity": 0.01, "FluidAlpha": 0.05, "SolidAlpha": 0.02,
                         "HeatFluxInObj": 1.0}
+    elif model == "d2q9_kuper_adj":
+        fl[:, 0, :] = nt("Wall")
+        fl[:, n - 1, :] = nt("Wall")
+        fl[:, 2:n // 2, n // 4 + 4:n // 4 + 8] |= nt("Obj1")
+        settings = {"InitDensity": 1.0, "WallDensity": 1.0, "Temperature": 0.56, "FAcc": 1.0, "Magic": 0.01,
+                    "MagicA": -0.152, "MagicF": 1.0, "GravitationX": 1e-4, "nu": 0.1, "FluidVelocityXInObj": 1.0,
+                    "Density1InObj": 0.1}
+    elif model == "d2q9_optimalMixing":
+        fl[:, 0, :] = nt("Wall")
+        fl[:, :, 0] = nt("Wall")
+        fl[:, :, n - 1] = nt("Wall")
+        fl[:, n - 1, 1:n - 1] = nt("NMovingWall") | mrt
+        settings = {"nu": 0.05, "K": 0.02, "MovingWallVelocity": 0.05, "Temperature": 1.0, "TotalTempSqrInObj": 1.0,
+                    "MovingWallPowerInObj": 0.1}
+    elif model == "d2q9_plate":
+        fl[:, 0, :] = nt("Wall")
+        fl[:, n - 1, :] = nt("Wall")
+        fl[:, 1:n - 1, 0] = nt("WVelocity") | mrt
+        fl[:, 1:n - 1, n - 1] = nt("EPressure") | mrt
+        settings = {"nu": 0.02, "VelocityX": 0.02, "Smag": 0.1, "PRAD": n / 16, "SM": 2.0, "PX": n / 4, "PY": n / 2,
+                    "ForceXInObj": 1.0, "PowerInObj": 0.5}
     else:
         raise SystemExit(f"no adjoint bench case for {model}")
     if m.node_type("DesignSpace") is not None:
@@ -79,9 +100,12 @@ def setup(model: str, n: int, dev):
     for k, v in settings.items():
         lat.set_setting(k, v)
     lat.init()
-    wi = m.field_index("w")
     f = lat.fields_interior().clone()
-    f[wi, :, :, 2:n // 4] = 0.7
+    if any(fd.nicename == "w" for fd in m.fields):
+        f[m.field_index("w"), :, :, 2:n // 4] = 0.7
+    if model == "d2q9_optimalMixing":        # a temperature pattern to mix: T = 1 in the lower half
+        for i in range(5):
+            f[m.field_index(f"g[{i}]"), :, : n // 2] *= 2.0
     lat.set_fields_interior(f)
     return lat
 
@@ -111,7 +135,8 @@ def main():
     ad.unsteady(a.steps)
     sync()
     ta = time.perf_counter() - t0
-    g = ad.field_gradient("w")
+    # models without a design field: the state adjoint of the initial condition
+    g = ad.field_gradient("w") if any(fd.nicename == "w" for fd in lat.model.fields) else ad.a0.cpu().numpy()
     nodes = lat.nodes
     ok = bool(np.isfinite(ad.J) and np.all(np.isfinite(g)))
     print(json.dumps({"case": f"{a.model} unsteady adjoint {'x'.join(map(str, lat.gshape))}", "device": a.device,
