@@ -69,6 +69,15 @@ addiag)
   for V in "" row row_o1 row_w1; do
     step "adjoint diag ${V:-flat}" 300 $O/adjoint_diag_${V:-flat}.jsonl env TCLB_AD_VARIANT=$V TCLB_NO_BUILD=1 python tools/adjoint_diag.py --repeats 2
   done ;;
+addiag2)
+  for V in "" row row_w2 row_w3; do
+    step "adjoint diag ${V:-flat}" 300 $O/adjoint_diag_${V:-flat}.jsonl env TCLB_AD_VARIANT=$V TCLB_NO_BUILD=1 python tools/adjoint_diag.py --repeats 2
+  done ;;
+adhost)
+  # host cost of an adjoint step: a lattice too small for the GPU time to matter
+  for M in d3q19_adj d3q19_heat_adj; do
+    step "adjoint host cost $M 16^3" 300 $O/adhost_${M}_16.json python tools/bench_adjoint.py --model $M --size 16 --steps 40
+  done ;;
 tiles)
   step "pf thermo 256 fp64 tiles vs nolds" 600 $O/tiles_thermo_256_fp64.jsonl python tools/perf_models.py --models d3q27_pf_velocity_thermo --n3 256 --steps 20 --variants ",nolds" --rounds 2 --allow-invalid
   step "pf 384 fp64 tiles vs nolds" 600 $O/tiles_pf384_fp64.jsonl python tools/perf_models.py --models d3q27_pf_velocity --n3 384 --steps 20 --variants ",nolds" --rounds 2 --allow-invalid

@@ -131,8 +131,13 @@ __device__ __forceinline__ void stage_body(const Launch& L) {
   const int x = L.xlo + (int)(t.x * blockDim.x + threadIdx.x);
   // blockDim.x is a multiple of 64 (launch_shape), so a wave covers 64 x of one row:
   // y is wave-uniform, and readfirstlane tells the compiler, which then keeps the row
-  // bases of every field in SGPRs (core.hpp row_at)
-  const int y = __builtin_amdgcn_readfirstlane(L.ylo + (int)(t.y * blockDim.y + threadIdx.y));
+  // bases of every field in SGPRs (core.hpp row_at).  Build variant "nru"
+  // (-DTCLB_UNIFORM_Y=0, with flat addresses): the round-2 form, for the headline A/B.
+#ifndef TCLB_UNIFORM_Y
+#define TCLB_UNIFORM_Y 1
+#endif
+  const int y = TCLB_UNIFORM_Y ? __builtin_amdgcn_readfirstlane(L.ylo + (int)(t.y * blockDim.y + threadIdx.y))
+                               : L.ylo + (int)(t.y * blockDim.y + threadIdx.y);
   const int z = L.zlo + (int)t.z;
   if constexpr (GLOB && !TCLB_GLOB_LDS) {
     constexpr int NG = Model::NGLOBALS_ > 0 ? Model::NGLOBALS_ : 1;
@@ -162,8 +167,19 @@ __device__ __forceinline__ void stage_body(const Launch& L) {
   }
 }
 
+// Occupancy floor of every stage kernel (build variant "sw2", -DTCLB_STAGE_WAVES=W): a
+// kernel just past 256 VGPRs runs at 1 wave/SIMD; the cap trades that for spills (A/B of
+// the register-heavy collisions, e.g. the tePSM CHT collide).  0 = no cap (default).
+#ifndef TCLB_STAGE_WAVES
+#define TCLB_STAGE_WAVES 0
+#endif
 template <class Model, class R, class S, int STG, bool GLOB>
-__global__ void __launch_bounds__(256) k_stage(const Launch L) {
+#if TCLB_STAGE_WAVES > 0
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TCLB_STAGE_WAVES)))
+#else
+__global__ void __launch_bounds__(256)
+#endif
+k_stage(const Launch L) {
   stage_body<Model, R, S, STG, GLOB>(L);
 }
 
