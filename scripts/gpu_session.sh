@@ -56,6 +56,12 @@ adbench2d)
 tepsm)
   step "tePSM 256 fp64 default vs sw2" 600 $O/tepsm_256_ab.jsonl python tools/perf_models.py --models d3q27_tePSM_per_NEBB --n3 256 --steps 20 --rounds 2 --variants ,sw2 --allow-invalid
   step "rocprof tePSM 256" 400 $O/prof_tepsm.log rocprofv3 --kernel-trace --stats -d $O/prof_tepsm -o run --output-format csv -- python3 $R/tools/perf_models.py --models d3q27_tePSM_per_NEBB --n3 256 --steps 10 ;;
+pfsw3)
+  step "pf 384 mixed-shift default vs sw3" 600 $O/pf384_ms_sw3.jsonl python tools/perf_models.py --models d3q27_pf_velocity --n3 384 --steps 20 --precision mixed-shift --variants ",sw3" --rounds 2 --allow-invalid
+  step "pf 384 fp64 default vs sw3" 600 $O/pf384_fp64_sw3.jsonl python tools/perf_models.py --models d3q27_pf_velocity --n3 384 --steps 20 --variants ",sw3" --rounds 2 --allow-invalid ;;
+tepsmsrc)
+  # srcA / srcB: the tePSM dynamics before 3debadf and without its closed-form stress
+  step "tePSM 256 fp64 source A/B" 600 $O/tepsm_256_src_ab.jsonl env TCLB_NO_BUILD=1 python tools/perf_models.py --models d3q27_tePSM_per_NEBB --n3 256 --steps 20 --rounds 2 --variants ",srcA,srcB" --allow-invalid ;;
 tiles2)
   step "pf 384 fp64" 600 $O/tiles2_pf384_fp64.jsonl python tools/perf_models.py --models d3q27_pf_velocity --n3 384 --steps 20 --rounds 2 --allow-invalid
   step "pf 384 mixed-shift" 600 $O/tiles2_pf384_ms.jsonl python tools/perf_models.py --models d3q27_pf_velocity --n3 384 --steps 20 --precision mixed-shift --rounds 2 --allow-invalid

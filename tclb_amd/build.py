@@ -50,14 +50,19 @@ VARIANTS = {
     # access instead of SGPR row base + 32-bit lane offset (core.hpp TCLB_ROW_ADDR=0)
     "gregs": ["-DTCLB_NT_STORE=1", "-DTCLB_GLOB_LDS=0"],
     "flataddr": ["-DTCLB_NT_STORE=1", "-DTCLB_ROW_ADDR=0"],
+    # the round-3 default: row addressing in the plain (globals-free) kernels too
+    "rowplain": ["-DTCLB_NT_STORE=1", "-DTCLB_ROW_ADDR_PLAIN=1"],
     # A/B of the LDS-staged stencil tiles (executor_hip.hpp k_tile): global loads instead
     "nolds": ["-DTCLB_NT_STORE=1", "-DTCLB_LDS_TILES=0"],
     # A/B of a 2-waves/SIMD floor on every stage kernel (executor_hip.hpp TCLB_STAGE_WAVES)
     "sw2": ["-DTCLB_NT_STORE=1", "-DTCLB_STAGE_WAVES=2"],
-    # headline A/B against the round-2 tree: flat addresses without the uniform-y hint
-    # ("nru"), and the flat node accessors of the adjoint build with register globals
-    "nru": ["-DTCLB_NT_STORE=1", "-DTCLB_ROW_ADDR=0", "-DTCLB_UNIFORM_Y=0"],
-    "flatnode": ["-DTCLB_NT_STORE=1", "-DTCLB_FLAT_NODE=1", "-DTCLB_GLOB_LDS=0"],
+    "sw3": ["-DTCLB_NT_STORE=1", "-DTCLB_STAGE_WAVES=3"],
+    # source A/B slots: the default flags, for a library built by hand from another
+    # revision of a model's dynamics (loaded with TCLB_NO_BUILD=1; profiles/README.md r04c)
+    "srcA": ["-DTCLB_NT_STORE=1", "-DTCLB_SRC_SLOT=1"],
+    "srcB": ["-DTCLB_NT_STORE=1", "-DTCLB_SRC_SLOT=2"],
+    # the round-2 form everywhere: flat accessors, register globals, no uniform-y hint
+    "r02like": ["-DTCLB_NT_STORE=1", "-DTCLB_FLAT_NODE=1", "-DTCLB_GLOB_LDS=0", "-DTCLB_UNIFORM_Y=0"],
 }
 DEFAULT_VARIANT = os.environ.get("TCLB_VARIANT", "")
 # CPU executor variants: "ubsan" builds the node code with UndefinedBehaviorSanitizer
