@@ -234,22 +234,34 @@ struct Addr {
 // sign-extended int each access needed its own 64-bit VGPR address (two VGPRs and a
 // v_lshl_add_u64 per load; 84 of them in the pf_velocity collide).  x < 2^28: a row is
 // shorter than a field.
-// Node accessors of the emitted model header: TCLB_FLAT_NODE=1 selects one flat index per
-// access and per-thread globals (the GPU adjoint build defines it, build.py _adhip_source)
+// TCLB_FLAT_NODE=1: the emitted node accessors take the flat form (one offset per access)
+// in every instantiation, the globals kernels included (the GPU adjoint build defines it,
+// build.py _adhip_source; emitter Node::ROWA_)
 #ifndef TCLB_FLAT_NODE
 #define TCLB_FLAT_NODE 0
 #endif
+// Which instantiations take the row form (ROW = true; the emitted Node passes ROWA_):
+// the globals-integrating (GLOB) stage kernels, where it keeps the accumulators' kernel
+// at 2 waves/SIMD (profiles/README.md r03o: +0.9 % instead of +11 % pf384 mixed-shift
+// with globals on every step); the plain kernels, the bulk of a run, take the 64-bit
+// flat address (row + x), which measured faster on the d3q27 headline (profiles/README.md
+// r04b/r04c, two boxes: +0.7-1.5 % fp64, +1.4-2 % mixed-shift).  TCLB_ROW_ADDR=0: flat
+// everywhere; TCLB_ROW_ADDR_PLAIN=1: the row form everywhere (the round-3 default).
 #ifndef TCLB_ROW_ADDR
 #define TCLB_ROW_ADDR 1
 #endif
-template <class T>
-TCLB_FN T* row_at(T* row, int x) {
-#if TCLB_GPU && defined(__HIP_DEVICE_COMPILE__) && TCLB_ROW_ADDR
-  typedef typename std::conditional<std::is_const<T>::value, const char, char>::type C;
-  return (T*)((C*)row + (unsigned)(x * (int)sizeof(T)));
-#else
-  return row + x;
+#ifndef TCLB_ROW_ADDR_PLAIN
+#define TCLB_ROW_ADDR_PLAIN 0
 #endif
+template <bool ROW, class T>
+TCLB_FN T* row_at(T* row, int x) {
+#if TCLB_GPU && defined(__HIP_DEVICE_COMPILE__)
+  if constexpr (ROW) {
+    typedef typename std::conditional<std::is_const<T>::value, const char, char>::type C;
+    return (T*)((C*)row + (unsigned)(x * (int)sizeof(T)));
+  }
+#endif
+  return row + x;
 }
 
 // Streaming loads/stores.  Every population is read once and written once per step,

@@ -130,14 +130,15 @@ __device__ __forceinline__ void stage_body(const Launch& L) {
   const uint3 t = tile_id();
   const int x = L.xlo + (int)(t.x * blockDim.x + threadIdx.x);
   // blockDim.x is a multiple of 64 (launch_shape), so a wave covers 64 x of one row:
-  // y is wave-uniform, and readfirstlane tells the compiler, which then keeps the row
-  // bases of every field in SGPRs (core.hpp row_at).  Build variant "nru"
-  // (-DTCLB_UNIFORM_Y=0, with flat addresses): the round-2 form, for the headline A/B.
+  // y is wave-uniform.  In the row-form instantiations (N::ROWA_, the globals kernels)
+  // readfirstlane tells the compiler, which then keeps the row bases of every field in
+  // SGPRs (core.hpp row_at); the flat-form plain kernels leave y in VGPRs, the form that
+  // measured fastest on the headline (profiles/README.md r04c).  -DTCLB_UNIFORM_Y=0: never.
 #ifndef TCLB_UNIFORM_Y
 #define TCLB_UNIFORM_Y 1
 #endif
-  const int y = TCLB_UNIFORM_Y ? __builtin_amdgcn_readfirstlane(L.ylo + (int)(t.y * blockDim.y + threadIdx.y))
-                               : L.ylo + (int)(t.y * blockDim.y + threadIdx.y);
+  const int y0 = L.ylo + (int)(t.y * blockDim.y + threadIdx.y);
+  const int y = (TCLB_UNIFORM_Y && N::ROWA_) ? __builtin_amdgcn_readfirstlane(y0) : y0;
   const int z = L.zlo + (int)t.z;
   if constexpr (GLOB && !TCLB_GLOB_LDS) {
     constexpr int NG = Model::NGLOBALS_ > 0 ? Model::NGLOBALS_ : 1;
