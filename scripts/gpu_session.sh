@@ -62,6 +62,11 @@ pfsw3)
 tepsmsrc)
   # srcA / srcB: the tePSM dynamics before 3debadf and without its closed-form stress
   step "tePSM 256 fp64 source A/B" 600 $O/tepsm_256_src_ab.jsonl env TCLB_NO_BUILD=1 python tools/perf_models.py --models d3q27_tePSM_per_NEBB --n3 256 --steps 20 --rounds 2 --variants ",srcA,srcB" --allow-invalid ;;
+kuperlds)
+  step "kuper / ShanChen LDS tiles vs nolds" 600 $O/kuper_lds_ab.jsonl python tools/perf_models.py --models d3q19_kuper,d2q9_kuper,d2q9_ShanChen --n3 256 --n2 4096 --steps 20 --rounds 2 --variants ",nolds" --allow-invalid ;;
+headab)
+  VARIANTS="r02 default rowplain r02like" bash scripts/headline_variants.sh 2 double mixed-shift
+  mkdir -p $O && cp $R/gpurun_out/ab/variants.log $O/headline_variants.log ;;
 tiles2)
   step "pf 384 fp64" 600 $O/tiles2_pf384_fp64.jsonl python tools/perf_models.py --models d3q27_pf_velocity --n3 384 --steps 20 --rounds 2 --allow-invalid
   step "pf 384 mixed-shift" 600 $O/tiles2_pf384_ms.jsonl python tools/perf_models.py --models d3q27_pf_velocity --n3 384 --steps 20 --precision mixed-shift --rounds 2 --allow-invalid

@@ -15,8 +15,9 @@ def build() -> Model:
     m.add_field("psi", stencil2d=1, group="pp")
     m.add_field("neighbour_type", stencil2d=1, group="neighbour_type_group")
     m.add_stage("BaseInit", "Init", save_fields=["f", "density", "neighbour_type_group"], load_densities=["f", "density"])
+    # the interaction force reads psi through a stencil: staged in LDS tiles on the GPU
     m.add_stage("BaseIteration", "Run", save_fields=["f", "density", "neighbour_type_group"],
-                load_densities=["f", "density", "neighbour_type_group"])
+                load_densities=["f", "density", "neighbour_type_group"], lds=["psi"])
     m.add_stage("PsiIteration", "calcPsi", save_fields=["psi"], load_densities=["f", "density"])
     m.add_action("Init", ["BaseInit", "PsiIteration"])
     m.add_action("Iteration", ["BaseIteration", "PsiIteration"])
