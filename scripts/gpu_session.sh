@@ -62,6 +62,11 @@ pfsw3)
 tepsmsrc)
   # srcA / srcB: the tePSM dynamics before 3debadf and without its closed-form stress
   step "tePSM 256 fp64 source A/B" 600 $O/tepsm_256_src_ab.jsonl env TCLB_NO_BUILD=1 python tools/perf_models.py --models d3q27_tePSM_per_NEBB --n3 256 --steps 20 --rounds 2 --variants ",srcA,srcB" --allow-invalid ;;
+rowab)
+  # plain kernels: flat offsets (default) vs the round-3 row form (rowplain) on the heavy models
+  step "pf384 ms flat vs rowplain" 600 $O/rowab_pf384_ms.jsonl python tools/perf_models.py --models d3q27_pf_velocity --n3 384 --steps 20 --precision mixed-shift --rounds 2 --variants ",rowplain" --allow-invalid
+  step "pf384 fp64 flat vs rowplain" 600 $O/rowab_pf384_fp64.jsonl python tools/perf_models.py --models d3q27_pf_velocity --n3 384 --steps 20 --rounds 2 --variants ",rowplain" --allow-invalid
+  step "heavy 256 flat vs rowplain" 900 $O/rowab_heavy_256.jsonl python tools/perf_models.py --models d3q27_tePSM_per_NEBB,d3q27_pf_velocity_thermo,d3q27q27_cm_cht,d3q19,d3q27_cumulant --n3 256 --steps 20 --rounds 2 --variants ",rowplain" --allow-invalid ;;
 kuperlds)
   step "kuper / ShanChen LDS tiles vs nolds" 600 $O/kuper_lds_ab.jsonl python tools/perf_models.py --models d3q19_kuper,d2q9_kuper,d2q9_ShanChen --n3 256 --n2 4096 --steps 20 --rounds 2 --variants ",nolds" --allow-invalid ;;
 headab)
