@@ -13,8 +13,9 @@ def build() -> Model:
     for i, (x, y) in enumerate(U9):
         m.add_density(f"f[{i}]", x, y, 0, group="f")
     m.add_field("phi", stencil2d=1)
-    # the interaction force reads phi through a stencil: staged in LDS tiles on the GPU
-    m.add_stage("BaseIteration", "Run", save_fields=["f"], load_densities=["f"], lds=["phi"])
+    # (an LDS tile of the phi stencil made the collision 2.5-9 % slower, profiles/README.md
+    # r04e: the stage streams all populations, so its tile marches one plane per group)
+    m.add_stage("BaseIteration", "Run", save_fields=["f"], load_densities=["f"])
     m.add_stage("CalcPhi", "CalcPhi", save_fields=["phi"], load_densities=["f"])
     m.add_stage("BaseInit", "Init", save_fields=["f"])
     m.add_action("Iteration", ["BaseIteration", "CalcPhi"])

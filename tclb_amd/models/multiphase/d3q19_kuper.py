@@ -17,8 +17,9 @@ def build() -> Model:
     for i in range(19):
         m.add_density(f"f[{i}]", int(U[i, 0]), int(U[i, 1]), int(U[i, 2]), group="f", comment=f"density F{i}")
     m.add_field("phi", stencil3d=1)
-    # the interaction force reads phi through a stencil: staged in LDS tiles on the GPU
-    m.add_stage("BaseIteration", "Run", save_fields=["f"], load_densities=["f"], lds=["phi"])
+    # (an LDS tile of the phi stencil made the collision 2.5-9 % slower, profiles/README.md
+    # r04e: the stage streams all populations, so its tile marches one plane per group)
+    m.add_stage("BaseIteration", "Run", save_fields=["f"], load_densities=["f"])
     m.add_stage("CalcPhi", "CalcPhi", save_fields=["phi"], load_densities=["f"])
     m.add_stage("BaseInit", "Init", save_fields=["f"])
     m.add_action("Iteration", ["BaseIteration", "CalcPhi"])
