@@ -127,6 +127,16 @@ def _deps(model_dir: str, dynamics: Optional[str]) -> List[str]:
 
 
 AD_HIP_DIR = os.path.join(CSRC, "include", "tclb_ad")
+TILE_DIR = os.path.join(CSRC, "include", "tclb_tile")
+
+
+def _tile_deps(model, kind: str) -> List[str]:
+    """the LDS-tile kernel headers (csrc/include/tclb_tile, included by executor_hip.hpp):
+    a dependency of the HIP libraries of models with LDS-staged stages only, so an edit of
+    the tile kernel rebuilds those and not the whole catalog"""
+    if kind != "hip" or not any(getattr(st, "lds", None) for st in model.stages):
+        return []
+    return [os.path.join(TILE_DIR, f) for f in sorted(os.listdir(TILE_DIR)) if f.endswith(".hpp")]
 
 
 def _adhip_source(model, gen_dir: str) -> str:
@@ -255,7 +265,7 @@ def source_stamp(name: str, kind: str, variant: str = "") -> str:
     gdir = os.path.join(BUILD, "gen", name)
     v = _variant_of(kind, variant)
     cmd = _cmd(kind, os.path.join(gdir, "kernels_" + kind), lib_path(name, kind, v), gdir, v)
-    deps = _deps_no_gen(model.dynamics) + (_ad_hip_deps() if kind == "adhip" else [])
+    deps = _deps_no_gen(model.dynamics) + (_ad_hip_deps() if kind == "adhip" else []) + _tile_deps(model, kind)
     return _rel_hash(deps, " ".join(cmd) + _python_stamp(name))
 
 
@@ -307,7 +317,8 @@ def build_model(name: str, kinds=("cpu", "hip"), force: bool = False, verbose: b
         target = lib_path(name, kind, v)
         src = _adhip_source(model, paths["dir"]) if kind == "adhip" else paths[kind]
         cmd = _cmd(kind, src, target, paths["dir"], v)
-        deps = _deps(paths["dir"], model.dynamics) + (_ad_hip_deps() if kind == "adhip" else [])
+        deps = (_deps(paths["dir"], model.dynamics) + (_ad_hip_deps() if kind == "adhip" else [])
+                + _tile_deps(model, kind))
         h = _hash_inputs(deps, " ".join(cmd))
         stamp = target + ".hash"
         if not force and os.path.exists(target) and os.path.exists(stamp) and open(stamp).read() == h:

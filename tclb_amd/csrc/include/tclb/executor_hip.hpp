@@ -213,104 +213,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W))) k
   stage_body<Model, R, S, STG, true>(L);
 }
 
-// LDS-staged stencil tiles (DSL Stage lds=[fields]; emitter tile tables tile_count /
-// tile_field / tile_h).  A stage whose node code reads scalar fields through a 3x3x3 (or
-// wider) stencil issues one global load per stencil point: 27+ loads per node per field,
-// served by L1/L2 but limited by the TA path at ~2-3 TB/s (profiles/README.md r02f LDS
-// A/B: 1.84 TB/s global vs 5.59 TB/s LDS).  k_tile instead marches a 64 x 4 work-group
-// through ZC z planes (Model::tile_zc: 16 for stencil-bound stages, 1 for stages that
-// also stream many populations): each plane of every staged field is loaded once into an LDS
-// ring of (2 hz + 1) planes of (64 + 2 hx) x (4 + 2 hy) elements (about 1.6 global loads
-// per node and field), and the node's reads of staged fields (the emitted ld()) come
-// from LDS.  Reads of other fields and every store stay global.  Results are the same as
-// k_stage's (the same node code reading the same values).
-#ifndef TCLB_LDS_TILES
-#define TCLB_LDS_TILES 1
-#endif
-
-template <class Model, class R, class S, int STG, bool GLOB>
-__global__ void __launch_bounds__(TILE_BX * TILE_BY) k_tile(const Launch L) {
-  typedef typename Model::template NodeTile<R, S, GLOB, STG> N;
-  typedef typename N::G_ G;
-  constexpr int NT = Model::tile_count(STG);
-  constexpr int TX = Model::tile_h(STG, 0), TY = Model::tile_h(STG, 1), TZ = Model::tile_h(STG, 2);
-  constexpr int W = TILE_BX + 2 * TX, H = TILE_BY + 2 * TY, NP = 2 * TZ + 1;
-  constexpr int PLANE = W * H, SLOT = NP * PLANE;
-  constexpr int NTH = TILE_BX * TILE_BY;
-  __shared__ S tile[NT * SLOT];
-  const int tx = threadIdx.x, ty = threadIdx.y, tid = tx + TILE_BX * ty;
-  const int x0 = L.xlo + (int)blockIdx.x * TILE_BX;
-  const int y0 = L.ylo + (int)blockIdx.y * TILE_BY;
-  constexpr int ZC = Model::tile_zc(STG);
-  const int zb = L.zlo + (int)blockIdx.z * ZC;
-  const int ze = zb + ZC < L.zhi ? zb + ZC : L.zhi;
-  const int x = x0 + tx;
-  const int y = __builtin_amdgcn_readfirstlane(y0 + ty);   // a wave is one row of the tile
-  const bool active = x < L.xhi && y < L.yhi;
-  const S* in = (const S*)L.in;
-  // plane z of every staged field into its ring slot; elements outside the snapshot
-  // (beyond a partial block's edge) are zero and never read by an active node
-  auto load_plane = [&](int z) {
-    const int ring = (z - zb + TZ) % NP;
-    int zz = z;
-    bool zok = true;
-    if (L.gz == 0) {
-      zok = z >= -L.nz && z < 2 * L.nz;
-      zz = wrap(z, L.nz);
-    } else {
-      zok = z >= -L.gz && z < L.nz + L.gz;
-    }
-    for (int i = tid; i < PLANE; i += NTH) {
-      const int ly = i / W, lx = i - ly * W;
-      int xx = x0 - TX + lx, yy = y0 - TY + ly;
-      bool ok = zok && xx < L.nx + TX && xx >= -TX;
-      xx = wrap(xx, L.nx);
-      if (L.gy == 0) {
-        ok = ok && yy >= -TY && yy < L.ny + TY;
-        yy = wrap(yy, L.ny);
-      } else {
-        ok = ok && yy >= -L.gy && yy < L.ny + L.gy;
-      }
-      const long long off = (long long)xx + L.sy * (long long)(yy + L.gy) + L.sz * (long long)(zz + L.gz);
-#pragma unroll
-      for (int k = 0; k < NT; k++) {
-        const int fi = Model::tile_field(STG, k);
-        tile[k * SLOT + ring * PLANE + i] = ok ? in[(long long)fi * L.fs + off] : S(0);
-      }
-    }
-  };
-  constexpr int NG = Model::NGLOBALS_ > 0 ? Model::NGLOBALS_ : 1;
-  __shared__ G acc[GLOB ? NG : 1];
-  if constexpr (GLOB) block_globals_init<NG, Model::NSUMGLOBALS_>(acc);
-  G g1[1] = {G(0)};
-  for (int z = zb - TZ; z < zb + TZ; z++) load_plane(z);
-  // ZC = 1 (stages whose node code is heavy: a z loop would let the compiler hoist the
-  // node's loop-invariant loads, e.g. every setting, and keep them live through the node)
-  for (int z = zb; ZC == 1 ? z == zb : z < ze; z++) {
-    load_plane(z + TZ);
-    __syncthreads();
-    if (active) {
-      // the LDS accumulators and the private dummy are separate constructions, so the
-      // address space of the node's globals pointer stays known (core.hpp glob_add)
-      auto run = [&](N& n) {
-        n.tile_ = tile;
-        n.tix_ = (ty + TY) * W + tx + TX;
-#pragma unroll
-        for (int d = 0; d < NP; d++) n.tpl_[d] = ((z + d - zb) % NP) * PLANE;
-        n.template run_stage<STG>();
-      };
-      if constexpr (GLOB) {
-        N n(L, x, y, z, acc);
-        run(n);
-      } else {
-        N n(L, x, y, z, g1);
-        run(n);
-      }
-    }
-    __syncthreads();   // the next plane load overwrites the ring slot read here
-  }
-  if constexpr (GLOB) block_globals_flush<NG, Model::NSUMGLOBALS_>(acc, L.globals);
-}
+// LDS-staged stencil tiles: csrc/include/tclb_tile/k_tile.hpp (a dependency of the
+// libraries of models with LDS-staged stages only, build.py _tile_deps)
+#include "tclb_tile/k_tile.hpp"
 
 template <class Model, class R, class S>
 __global__ void __launch_bounds__(256) k_quantity(const Launch L) {
