@@ -23,6 +23,11 @@ pfcounters) step "counters pf384 mixed-shift" 500 $O/counters_pf384_ms.log pytho
 modelcounters)
   step "counters stencil models" 600 $O/counters_models.log python tools/counters.py --tag models_16M --nodes 16777216 --outdir $O/counters -- python3 $R/tools/perf_models.py --models d3q27_PSM_NEBB,d2q9_ShanChen,d2q9_kuper --steps 5
   step "counters part256" 500 $O/counters_part256.log python tools/counters.py --tag part256_fp64 --nodes 16777216 --outdir $O/counters -- python3 $R/tools/bench_configs.py --configs part256 --steps 5 --warmup 1 ;;
+final)
+  step "bench fp64" 300 $O/bench_fp64.json python bench.py
+  step "bench fp64 100 steps" 300 $O/bench_fp64_100.json python bench.py --steps 100 --warmup 10
+  step "bench mixed-shift 100 steps" 300 $O/bench_ms_100.json python bench.py --steps 100 --warmup 10 --precision mixed-shift
+  step "rocprof fp64 headline" 400 $O/prof_fp64.log rocprofv3 --kernel-trace --stats -d $O/prof_fp64 -o run --output-format csv -- python3 $R/bench.py --steps 20 --warmup 2 ;;
 thermo)
   step "pf thermo 256 fp64" 600 $O/thermo_256_fp64.jsonl python tools/perf_models.py --models d3q27_pf_velocity_thermo,d2q9_ShanChen --n3 256 --n2 4096 --steps 20 --rounds 2 --allow-invalid
   step "rocprof pf thermo 256" 400 $O/prof_thermo.log rocprofv3 --kernel-trace --stats -d $O/prof_thermo -o run --output-format csv -- python3 $R/tools/perf_models.py --models d3q27_pf_velocity_thermo --n3 256 --steps 10 ;;
