@@ -23,6 +23,12 @@ pfcounters) step "counters pf384 mixed-shift" 500 $O/counters_pf384_ms.log pytho
 modelcounters)
   step "counters stencil models" 600 $O/counters_models.log python tools/counters.py --tag models_16M --nodes 16777216 --outdir $O/counters -- python3 $R/tools/perf_models.py --models d3q27_PSM_NEBB,d2q9_ShanChen,d2q9_kuper --steps 5
   step "counters part256" 500 $O/counters_part256.log python tools/counters.py --tag part256_fp64 --nodes 16777216 --outdir $O/counters -- python3 $R/tools/bench_configs.py --configs part256 --steps 5 --warmup 1 ;;
+slabhost)
+  # host cost of a native multi-rank step (launches, events, RCCL group calls) against its
+  # GPU time, on the 8-GPU per-rank slab
+  for P in mixed-shift double; do
+    step "slab $P native rccl self" 300 $O/slab_${P}_rccl.json python bench.py --shape 512,512,64 --precision $P --steps 200 --warmup 20 --loopback-dist --transport rccl
+  done ;;
 final)
   step "bench fp64" 300 $O/bench_fp64.json python bench.py
   step "bench fp64 100 steps" 300 $O/bench_fp64_100.json python bench.py --steps 100 --warmup 10
