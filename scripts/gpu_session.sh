@@ -76,9 +76,6 @@ tepsm)
 pfsw3)
   step "pf 384 mixed-shift default vs sw3" 600 $O/pf384_ms_sw3.jsonl python tools/perf_models.py --models d3q27_pf_velocity --n3 384 --steps 20 --precision mixed-shift --variants ",sw3" --rounds 2 --allow-invalid
   step "pf 384 fp64 default vs sw3" 600 $O/pf384_fp64_sw3.jsonl python tools/perf_models.py --models d3q27_pf_velocity --n3 384 --steps 20 --variants ",sw3" --rounds 2 --allow-invalid ;;
-tepsmsrc)
-  # srcA / srcB: the tePSM dynamics before 3debadf and without its closed-form stress
-  step "tePSM 256 fp64 source A/B" 600 $O/tepsm_256_src_ab.jsonl env TCLB_NO_BUILD=1 python tools/perf_models.py --models d3q27_tePSM_per_NEBB --n3 256 --steps 20 --rounds 2 --variants ",srcA,srcB" --allow-invalid ;;
 rowab)
   # plain kernels: flat offsets (default) vs the round-3 row form (rowplain) on the heavy models
   step "pf384 ms flat vs rowplain" 600 $O/rowab_pf384_ms.jsonl python tools/perf_models.py --models d3q27_pf_velocity --n3 384 --steps 20 --precision mixed-shift --rounds 2 --variants ",rowplain" --allow-invalid

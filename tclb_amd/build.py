@@ -57,10 +57,6 @@ VARIANTS = {
     # A/B of a 2-waves/SIMD floor on every stage kernel (executor_hip.hpp TCLB_STAGE_WAVES)
     "sw2": ["-DTCLB_NT_STORE=1", "-DTCLB_STAGE_WAVES=2"],
     "sw3": ["-DTCLB_NT_STORE=1", "-DTCLB_STAGE_WAVES=3"],
-    # source A/B slots: the default flags, for a library built by hand from another
-    # revision of a model's dynamics (loaded with TCLB_NO_BUILD=1; profiles/README.md r04c)
-    "srcA": ["-DTCLB_NT_STORE=1", "-DTCLB_SRC_SLOT=1"],
-    "srcB": ["-DTCLB_NT_STORE=1", "-DTCLB_SRC_SLOT=2"],
     # the round-2 form everywhere: flat accessors, register globals, no uniform-y hint
     "r02like": ["-DTCLB_NT_STORE=1", "-DTCLB_FLAT_NODE=1", "-DTCLB_GLOB_LDS=0", "-DTCLB_UNIFORM_Y=0"],
 }
