@@ -29,6 +29,9 @@ slabhost)
   for P in mixed-shift double; do
     step "slab $P native rccl self" 300 $O/slab_${P}_rccl.json python bench.py --shape 512,512,64 --precision $P --steps 200 --warmup 20 --loopback-dist --transport rccl
   done ;;
+headab2)
+  VARIANTS="default xcd nt mclause" bash scripts/headline_variants.sh 2 double mixed-shift
+  mkdir -p $O && cp $R/gpurun_out/ab/variants.log $O/headline_variants.log ;;
 final)
   step "bench fp64" 300 $O/bench_fp64.json python bench.py
   step "bench fp64 100 steps" 300 $O/bench_fp64_100.json python bench.py --steps 100 --warmup 10

@@ -58,6 +58,8 @@ VARIANTS = {
     "sw2": ["-DTCLB_NT_STORE=1", "-DTCLB_STAGE_WAVES=2"],
     "sw3": ["-DTCLB_NT_STORE=1", "-DTCLB_STAGE_WAVES=3"],
     # the round-2 form everywhere: flat accessors, register globals, no uniform-y hint
+    # scheduler A/B: memory clauses grouped by the AMDGPU machine scheduler
+    "mclause": ["-DTCLB_NT_STORE=1", "-mllvm", "-amdgpu-sched-strategy=max-memory-clause"],
     "r02like": ["-DTCLB_NT_STORE=1", "-DTCLB_FLAT_NODE=1", "-DTCLB_GLOB_LDS=0", "-DTCLB_UNIFORM_Y=0"],
 }
 DEFAULT_VARIANT = os.environ.get("TCLB_VARIANT", "")
