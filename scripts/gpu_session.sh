@@ -37,6 +37,11 @@ xcdab)
   mkdir -p $O && cp $R/gpurun_out/ab/variants.log $O/headline_variants.log
   step "models fp64 default vs xcd" 900 $O/xcd_models_fp64.jsonl python tools/perf_models.py --models d3q27_cumulant,d3q19,d3q27_tePSM_per_NEBB,d3q27q27_cm_cht,d3q27_pf_velocity_thermo --n3 256 --steps 20 --rounds 2 --variants ",xcd" --allow-invalid
   step "pf384 fp64 / ms default vs xcd" 900 $O/xcd_pf384.jsonl bash -c 'python tools/perf_models.py --models d3q27_pf_velocity --n3 384 --steps 20 --rounds 2 --variants ",xcd" --allow-invalid && python tools/perf_models.py --models d3q27_pf_velocity --n3 384 --steps 20 --rounds 2 --precision mixed-shift --variants ",xcd" --allow-invalid' ;;
+xcdsize)
+  for r in 1 2; do for n in 384 448 512; do for v in "" xcd; do
+    step "d3q27 fp64 $n ${v:-default}" 300 $O/xcd_size_${n}_${v:-default}_$r.json env TCLB_VARIANT=$v TCLB_NO_BUILD=1 python bench.py --size $n --steps 50 --warmup 5
+  done; done; done
+  step "d3q19 fp64 512 default vs xcd" 600 $O/xcd_d3q19_512.jsonl python tools/perf_models.py --models d3q19,d3q27_cumulant --n3 512 --steps 20 --rounds 2 --variants ",xcd" --allow-invalid ;;
 final)
   step "bench fp64" 300 $O/bench_fp64.json python bench.py
   step "bench fp64 100 steps" 300 $O/bench_fp64_100.json python bench.py --steps 100 --warmup 10
