@@ -42,6 +42,13 @@ xcdsize)
     step "d3q27 fp64 $n ${v:-default}" 300 $O/xcd_size_${n}_${v:-default}_$r.json env TCLB_VARIANT=$v TCLB_NO_BUILD=1 python bench.py --size $n --steps 50 --warmup 5
   done; done; done
   step "d3q19 fp64 512 default vs xcd" 600 $O/xcd_d3q19_512.jsonl python tools/perf_models.py --models d3q19,d3q27_cumulant --n3 512 --steps 20 --rounds 2 --variants ",xcd" --allow-invalid ;;
+padab)
+  # row pitch / field padding of the 512^3 headline (runtime layout knobs, no rebuild)
+  for r in 1 2; do for P in double mixed-shift; do
+    for cfg in "0 0" "64 0" "128 0" "0 4096" "64 4096"; do set -- $cfg
+      step "pad x=$1 f=$2 $P" 300 $O/pad_${P}_x$1_f$2_$r.json env TCLB_X_PAD=$1 TCLB_FIELD_PAD=$2 python bench.py --steps 50 --warmup 5 --precision $P
+    done
+  done; done ;;
 final)
   step "bench fp64" 300 $O/bench_fp64.json python bench.py
   step "bench fp64 100 steps" 300 $O/bench_fp64_100.json python bench.py --steps 100 --warmup 10

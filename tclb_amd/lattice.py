@@ -92,6 +92,11 @@ class Lattice:
         if ax == 2 and hy > ny:
             raise ValueError("y stencil larger than domain")
         self.px = ((nx + 63) // 64) * 64 if nx >= 64 else ((nx + 7) // 8) * 8
+        # optional extra x pitch (elements, a multiple of 64, env TCLB_X_PAD): moves the
+        # rows of power-of-two lattices off a common HBM channel stride; 0 = none
+        xpad = int(os.environ.get("TCLB_X_PAD", "0"))
+        if xpad and nx >= 64:
+            self.px += (xpad + 63) // 64 * 64
         self.NY = ny + 2 * self.gy
         self.NZ = nz + 2 * self.gz
         self.device = torch.device(device) if device is not None else torch.device("cpu")
