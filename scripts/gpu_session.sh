@@ -49,6 +49,15 @@ padab)
       step "pad x=$1 f=$2 $P" 300 $O/pad_${P}_x$1_f$2_$r.json env TCLB_X_PAD=$1 TCLB_FIELD_PAD=$2 python bench.py --steps 50 --warmup 5 --precision $P
     done
   done; done ;;
+padab2)
+  for r in 1 2 3; do
+    for x in 0 128 192 256; do
+      step "pad x=$x fp64" 300 $O/pad2_double_x${x}_$r.json env TCLB_X_PAD=$x python bench.py --steps 50 --warmup 5
+    done
+    for x in 0 128; do
+      step "pad x=$x ms" 300 $O/pad2_ms_x${x}_$r.json env TCLB_X_PAD=$x python bench.py --steps 50 --warmup 5 --precision mixed-shift
+    done
+  done ;;
 final)
   step "bench fp64" 300 $O/bench_fp64.json python bench.py
   step "bench fp64 100 steps" 300 $O/bench_fp64_100.json python bench.py --steps 100 --warmup 10
