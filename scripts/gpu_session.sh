@@ -61,6 +61,9 @@ padab2)
 pfdroplet)
   step "rocprof pf384 droplet ms" 400 $O/prof_pf384_droplet_ms.log rocprofv3 --kernel-trace --stats -d $O/prof_pf384_droplet_ms -o run --output-format csv -- python3 $R/tools/bench_configs.py --configs pf384 --steps 10 --warmup 2 --precision mixed-shift
   step "rocprof pf384 uniform ms" 400 $O/prof_pf384_uniform_ms.log rocprofv3 --kernel-trace --stats -d $O/prof_pf384_uniform_ms -o run --output-format csv -- python3 $R/tools/perf_models.py --models d3q27_pf_velocity --n3 384 --steps 10 --precision mixed-shift ;;
+pfcount2)
+  step "counters pf384 droplet ms" 500 $O/counters_droplet.log python tools/counters.py --tag pf384_droplet_ms --nodes 56623104 --outdir $O/counters -- python3 $R/tools/bench_configs.py --configs pf384 --steps 5 --warmup 1 --precision mixed-shift
+  step "counters pf384 uniform ms" 500 $O/counters_uniform.log python tools/counters.py --tag pf384_uniform_ms --nodes 56623104 --outdir $O/counters -- python3 $R/tools/perf_models.py --models d3q27_pf_velocity --n3 384 --steps 5 --precision mixed-shift ;;
 final)
   step "bench fp64" 300 $O/bench_fp64.json python bench.py
   step "bench fp64 100 steps" 300 $O/bench_fp64_100.json python bench.py --steps 100 --warmup 10
