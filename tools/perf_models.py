@@ -25,6 +25,20 @@ def state_finite(lat) -> bool:
     return all(bool(torch.isfinite(s[i]).all().item()) for i in range(lat.nf))
 
 
+def collision_flag(m) -> int:
+    """the node-type value of the collision the model's default build runs: MRT where the
+    model has both BGK and MRT types and is not built with its BGK option (the first
+    COLLISION type alone flagged d3q27_pf_velocity(_thermo) BGK, which their MRT build
+    does not collide: those runs streamed only, profiles/README.md r04r)"""
+    types = [n for n in m.node_types if n.group == "COLLISION"]
+    if not types:
+        return 0
+    names = [n.name for n in types]
+    if "MRT" in names and not (getattr(m, "options", None) or {}).get("BGK"):
+        return types[names.index("MRT")].value
+    return types[0].value
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--models", default="")
@@ -46,7 +60,7 @@ def main():
         shape = (a.n3, a.n3, a.n3) if m.dims == 3 else (a.n2, a.n2, 1)
         try:
             lat = Lattice(name, shape, device=dev, precision=a.precision, variant=variant)
-            coll = next((n.value for n in m.node_types if n.group == "COLLISION"), 0)
+            coll = collision_flag(m)
             lat.set_flags(np.full((lat.NZ, lat.NY, shape[0]), coll, dtype=np.uint32))
             # the model-family settings of the catalog tests (a physical case; some
             # defaults, e.g. zero densities of the phase-field models, are not)
