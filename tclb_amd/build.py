@@ -155,7 +155,9 @@ def _adhip_source(model, gen_dir: str) -> str:
     return p
 
 
-def _cmd(kind: str, src: str, out: str, gen_dir: str, variant: str = "") -> List[str]:
+def _cmd(kind: str, src: str, out: str, gen_dir: str, variant: str = "", model_flags=()) -> List[str]:
+    """the compile command of one library; model_flags: the model's own HIP defines
+    (Model.hip_flags, e.g. the addressing form its collide measured faster with)"""
     incs = ["-I", os.path.join(CSRC, "include"), "-I", os.path.join(CSRC, "models"), "-I", gen_dir]
     if kind == "adhip":
         return [HIPCC, f"--offload-arch={ARCH}", "-O2", "-std=c++17", "-fPIC", "-shared", "-munsafe-fp-atomics",
@@ -170,7 +172,7 @@ def _cmd(kind: str, src: str, out: str, gen_dir: str, variant: str = "") -> List
                 # AddTo<global> into LDS (core.hpp glob_add): a DPP wave reduction + one
                 # LDS atomic per wave instead of the default lane-by-lane loop
                 "-mllvm", "-amdgpu-atomic-optimizer-strategy=DPP",
-                "-Wno-unused-result", "-Wno-pass-failed", *VARIANTS[variant], *incs,
+                "-Wno-unused-result", "-Wno-pass-failed", *model_flags, *VARIANTS[variant], *incs,
                 src, "-o", out]
     opt = "-O2" if kind == "ad" else "-O3"
     extra = CPU_VARIANTS.get(variant, []) if kind == "cpu" else []
@@ -262,7 +264,8 @@ def source_stamp(name: str, kind: str, variant: str = "") -> str:
     model = registry.get(name)
     gdir = os.path.join(BUILD, "gen", name)
     v = _variant_of(kind, variant)
-    cmd = _cmd(kind, os.path.join(gdir, "kernels_" + kind), lib_path(name, kind, v), gdir, v)
+    cmd = _cmd(kind, os.path.join(gdir, "kernels_" + kind), lib_path(name, kind, v), gdir, v,
+               getattr(model, "hip_flags", ()))
     deps = _deps_no_gen(model.dynamics) + (_ad_hip_deps() if kind == "adhip" else []) + _tile_deps(model, kind)
     return _rel_hash(deps, " ".join(cmd) + _python_stamp(name))
 
@@ -314,7 +317,7 @@ def build_model(name: str, kinds=("cpu", "hip"), force: bool = False, verbose: b
         v = _variant_of(kind, variant)
         target = lib_path(name, kind, v)
         src = _adhip_source(model, paths["dir"]) if kind == "adhip" else paths[kind]
-        cmd = _cmd(kind, src, target, paths["dir"], v)
+        cmd = _cmd(kind, src, target, paths["dir"], v, getattr(model, "hip_flags", ()))
         deps = (_deps(paths["dir"], model.dynamics) + (_ad_hip_deps() if kind == "adhip" else [])
                 + _tile_deps(model, kind))
         h = _hash_inputs(deps, " ".join(cmd))
