@@ -69,6 +69,8 @@ pfmrt)
   step "pf384 MRT ms/fp64 default vs rowplain" 900 $O/pf384_mrt.jsonl bash -c 'python tools/perf_models.py --models d3q27_pf_velocity --n3 384 --steps 20 --rounds 2 --precision mixed-shift --variants ",rowplain" --allow-invalid && python tools/perf_models.py --models d3q27_pf_velocity --n3 384 --steps 20 --rounds 2 --variants ",rowplain" --allow-invalid'
   step "thermo 256 MRT default vs rowplain" 600 $O/thermo_mrt.jsonl python tools/perf_models.py --models d3q27_pf_velocity_thermo,d2q9_kuper --n3 256 --n2 4096 --steps 20 --rounds 2 --variants ",rowplain" --allow-invalid
   step "rocprof thermo 256 MRT" 400 $O/prof_thermo_mrt.log rocprofv3 --kernel-trace --stats -d $O/prof_thermo_mrt -o run --output-format csv -- python3 $R/tools/perf_models.py --models d3q27_pf_velocity_thermo --n3 256 --steps 10 ;;
+thermofinal)
+  step "thermo 256 MRT" 600 $O/thermo_mrt_final.jsonl python tools/perf_models.py --models d3q27_pf_velocity_thermo --n3 256 --steps 20 --rounds 2 --allow-invalid ;;
 final)
   step "bench fp64" 300 $O/bench_fp64.json python bench.py
   step "bench fp64 100 steps" 300 $O/bench_fp64_100.json python bench.py --steps 100 --warmup 10
