@@ -174,17 +174,24 @@ def main():
     lat.iterate(4, glob_last=False)
     t_enqueue = (time.perf_counter() - th) / 4
     sync()
+    it0 = lat.iter
     t0 = time.perf_counter()
     if a.glob_every_step:
         for _ in range(a.steps):
             lat.iterate(1, glob_last=True)
         t_host = time.perf_counter() - t0
     else:
-        lat.iterate(a.steps, glob_last=False) if a.steps > 1 else None
+        # exactly `steps` iterations in the window: steps - 1 plain ones, then the last
+        # with the globals integrated (as Lattice::Iterate does on its last iteration)
+        if a.steps > 1:
+            lat.iterate(a.steps - 1, glob_last=False)
         t_host = time.perf_counter() - t0       # the host's enqueue time of the window
-        lat.iterate(1, glob_last=True) if a.steps > 1 else lat.iterate(a.steps, glob_last=True)
+        lat.iterate(1, glob_last=True)
     sync()
     dt = time.perf_counter() - t0
+    iters_timed = lat.iter - it0
+    if iters_timed != a.steps:
+        raise SystemExit(f"bench.py: {iters_timed} iterations in the timed window, expected {a.steps}")
     dt = comm.allreduce_scalar(dt, "max")
     t_host = comm.allreduce_scalar(t_host, "max")
     nodes = shape[0] * shape[1] * shape[2]
@@ -217,6 +224,7 @@ def main():
             "effective_GBps_per_gpu": round(mlups * bytes_node / 1e3 / world, 1),
             "globals_finite": chk["globals_finite"],
             "checks": chk,
+            "iterations_timed": iters_timed,
             "host_ms_per_step": round(t_host / max(1, a.steps - 1) * 1e3, 4) if not a.glob_every_step else None,
             "host_enqueue_ms_per_step": round(t_enqueue * 1e3, 4),
             "loop": ("native-dist/" + lat._dist.transport) if lat._dist is not None else

@@ -26,6 +26,7 @@ def test_bench_two_ranks_json_line():
     base = json.load(open(os.path.join(ROOT, "BASELINE.json")))
     out = _run(2, 29611)
     assert out["n_gpus"] == 2 and out["steps"] == 3 and out["warmup"] == 1
+    assert out["iterations_timed"] == 3            # the window holds exactly `steps` iterations
     assert out["value"] > 0 and out["higher_is_better"] is True
     assert out["config"]["parallelism"] == "zslab2"
     assert out["globals_finite"] is True
@@ -59,3 +60,20 @@ def test_bench_rejects_rank_count_mismatch():
            "--steps", "1", "--warmup", "0"]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=120, env=env, cwd=ROOT)
     assert r.returncode == 2 and "WORLD_SIZE=2" in r.stderr
+
+
+def test_bench_window_holds_exactly_steps_iterations():
+    """one rank: the timed window runs exactly --steps iterations (steps - 1 plain, the last
+    with globals), so MLUPS = nodes * steps / window is not under-reported (round-4 bug:
+    steps + 1 iterations over a steps divisor)"""
+    env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="2")
+    env.pop("WORLD_SIZE", None)
+    for steps in (1, 4):
+        cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--cpu", "--shape", "32,16,16",
+               "--steps", str(steps), "--warmup", "1"]
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
+        assert r.returncode == 0, r.stderr[-3000:]
+        out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
+        assert out["iterations_timed"] == steps and out["steps"] == steps
+        window = 32 * 16 * 16 * steps / (out["value"] * 1e6)          # seconds, from the MLUPS
+        assert abs(out["ms_per_step"] * steps / 1e3 - window) <= 0.01 * window + 1e-7
