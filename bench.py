@@ -167,6 +167,10 @@ def main():
         comm.barrier()
 
     lat.iterate(a.warmup, glob_last=False)
+    if os.environ.get("TCLB_BENCH_FAIL_RANK") == str(rank):
+        # failure drill (tests/test_bench_contract.py): this rank dies while the others
+        # wait in the barrier below; the launcher must end the job, not hang
+        raise SystemExit(f"bench.py: rank {rank} failing on purpose (TCLB_BENCH_FAIL_RANK)")
     sync()
     # host cost of a step on an idle queue: the enqueue time of a few steps (launches,
     # events, RCCL group calls) before the GPU has caught up — outside the timed window
@@ -227,8 +231,8 @@ def main():
             "iterations_timed": iters_timed,
             "host_ms_per_step": round(t_host / max(1, a.steps - 1) * 1e3, 4) if not a.glob_every_step else None,
             "host_enqueue_ms_per_step": round(t_enqueue * 1e3, 4),
-            "loop": ("native-dist/" + lat._dist.transport) if lat._dist is not None else
-                    ("native" if lat._native_ok("Iteration") else "python"),
+            "loop": ("native-dist/" + lat._dist.transport) if (lat._dist is not None and lat.comm.distributed) else
+                    {"lib": "native", "loop": "native-loop", None: "python"}[lat._native_path("Iteration")],
             "baseline_note": "reference publishes no MLUPS (BASELINE.md); vs_baseline null",
         }
         print(json.dumps(out), flush=True)

@@ -277,7 +277,7 @@ class Adjoint:
 
     # ------------------------------------------------------------------ unsteady
     def unsteady(self, steps: int, action: str = "Iteration", checkpoint: int = 0,
-                 a_final: Optional[torch.Tensor] = None) -> torch.Tensor:
+                 a_final: Optional[torch.Tensor] = None, keep_segment: Optional[bool] = None) -> torch.Tensor:
         """run `steps` primal iterations from the current state recording checkpoints,
         then sweep backwards; returns dJ/d(initial state).  The primal ends at its final
         state (as the reference's record/rewind leaves it).
@@ -293,7 +293,8 @@ class Adjoint:
         # not fit in half the free memory, keep only checkpoints and re-run each reverse
         # step from its checkpoint instead (no segment states)
         snap_bytes = lat.snaps[0].numel() * lat.snaps[0].element_size()
-        keep_segment = (steps // checkpoint + checkpoint + 2) * snap_bytes <= 0.5 * self._free_bytes()
+        if keep_segment is None:
+            keep_segment = (steps // checkpoint + checkpoint + 2) * snap_bytes <= 0.5 * self._free_bytes()
         it0 = lat.iter
         snaps: Dict[int, torch.Tensor] = {0: lat.snaps[lat.cur].clone()}
         # with late reads (Model.late_reads) a step also depends on what its output
@@ -329,7 +330,12 @@ class Adjoint:
             # overwrites the whole interior: the recompute buffers need no zero fill
             uninit = not lat.ghosts and lat.writes_all_fields(action)
             for t in range(base + 1, end if keep_segment else base + 1):
-                lat.snaps[1 - lat.cur] = lat.new_snapshot(uninit)
+                if late:
+                    # the step reads what its output snapshot held in the primal run: the
+                    # state two steps back (prev[base] before the segment's first step)
+                    lat.snaps[1 - lat.cur] = (states[-2] if len(states) > 1 else prev[base]).clone()
+                else:
+                    lat.snaps[1 - lat.cur] = lat.new_snapshot(uninit)
                 lat.iterate(1, glob_last=False, action=action)
                 states.append(lat.snaps[lat.cur])
             for t in range(end - 1, base - 1, -1):

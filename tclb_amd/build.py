@@ -35,7 +35,6 @@ VARIANTS = {
     "nt": ["-DTCLB_NT_LOAD=1", "-DTCLB_NT_STORE=1"],
     "ntld": ["-DTCLB_NT_LOAD=1"],
     "noxs": ["-DTCLB_DEBUG_NO_XSHIFT", "-DTCLB_NT_STORE=1"],   # diagnostic: aligned-x ceiling
-    "xcd": ["-DTCLB_NT_STORE=1", "-DTCLB_XCD_REMAP=1"],        # XCD-contiguous block->tile map
     # occupancy floor for the fp32/fp16-storage kernels (executor_hip.hpp k_stage_narrow)
     "nw3": ["-DTCLB_NT_STORE=1", "-DTCLB_NARROW_WAVES=3"],
     "nw4": ["-DTCLB_NT_STORE=1", "-DTCLB_NARROW_WAVES=4"],
@@ -101,9 +100,19 @@ def _hash_inputs(paths: Iterable[str], extra: str = "") -> str:
     return h.hexdigest()
 
 
-def _deps(model_dir: str, dynamics: Optional[str]) -> List[str]:
+# executor headers: each is included by the instantiation of one library kind only
+# (kernels_<kind> of the emitted model), so an edit of one rebuilds that kind alone
+_EXECUTOR_OF = {"executor_hip.hpp": ("hip",), "executor_cpu.hpp": ("cpu",), "executor_ad.hpp": ("ad",)}
+
+
+def _tclb_headers(kind: Optional[str]) -> List[str]:
     inc = os.path.join(CSRC, "include", "tclb")
-    deps = [os.path.join(inc, f) for f in os.listdir(inc) if f.endswith((".hpp", ".h"))]
+    return [os.path.join(inc, f) for f in sorted(os.listdir(inc)) if f.endswith((".hpp", ".h"))
+            and (kind is None or kind in _EXECUTOR_OF.get(f, (kind,)))]
+
+
+def _deps(model_dir: str, dynamics: Optional[str], kind: Optional[str] = None) -> List[str]:
+    deps = _tclb_headers(kind)
     deps += [os.path.join(model_dir, f) for f in os.listdir(model_dir)
              if f.endswith((".hpp", ".hip", ".cpp")) and f != "kernels_adhip.hip"]
     # the dynamics include and everything it includes from csrc/models (transitively)
@@ -266,7 +275,7 @@ def source_stamp(name: str, kind: str, variant: str = "") -> str:
     v = _variant_of(kind, variant)
     cmd = _cmd(kind, os.path.join(gdir, "kernels_" + kind), lib_path(name, kind, v), gdir, v,
                getattr(model, "hip_flags", ()))
-    deps = _deps_no_gen(model.dynamics) + (_ad_hip_deps() if kind == "adhip" else []) + _tile_deps(model, kind)
+    deps = _deps_no_gen(model.dynamics, kind) + (_ad_hip_deps() if kind == "adhip" else []) + _tile_deps(model, kind)
     return _rel_hash(deps, " ".join(cmd) + _python_stamp(name))
 
 
@@ -274,9 +283,8 @@ def _ad_hip_deps() -> List[str]:
     return [os.path.join(AD_HIP_DIR, f) for f in sorted(os.listdir(AD_HIP_DIR)) if f.endswith(".hpp")]
 
 
-def _deps_no_gen(dynamics: Optional[str]) -> List[str]:
-    inc = os.path.join(CSRC, "include", "tclb")
-    deps = [os.path.join(inc, f) for f in os.listdir(inc) if f.endswith((".hpp", ".h"))]
+def _deps_no_gen(dynamics: Optional[str], kind: Optional[str] = None) -> List[str]:
+    deps = _tclb_headers(kind)
     todo, seen = ([dynamics] if dynamics else []), set()
     while todo:
         rel = todo.pop()
@@ -318,7 +326,7 @@ def build_model(name: str, kinds=("cpu", "hip"), force: bool = False, verbose: b
         target = lib_path(name, kind, v)
         src = _adhip_source(model, paths["dir"]) if kind == "adhip" else paths[kind]
         cmd = _cmd(kind, src, target, paths["dir"], v, getattr(model, "hip_flags", ()))
-        deps = (_deps(paths["dir"], model.dynamics) + (_ad_hip_deps() if kind == "adhip" else [])
+        deps = (_deps(paths["dir"], model.dynamics, kind) + (_ad_hip_deps() if kind == "adhip" else [])
                 + _tile_deps(model, kind))
         h = _hash_inputs(deps, " ".join(cmd))
         stamp = target + ".hash"
@@ -369,12 +377,16 @@ def host_runtime_stale() -> Optional[str]:
         return "missing"
     rdir = os.path.join(CSRC, "runtime")
     srcs = sorted(os.path.join(rdir, f) for f in os.listdir(rdir) if f.endswith(".cpp"))
-    cmd = [CXX, "-O3", "-std=c++17", "-fPIC", "-shared", "-fopenmp", "-I", os.path.join(CSRC, "include"),
-           *srcs, "-lz", "-o", target + ".tmp"]
     stamp = target + ".hash"
-    if not os.path.exists(stamp) or open(stamp).read() != _hash_inputs(srcs + _rt_headers(), " ".join(cmd)):
+    if not os.path.exists(stamp) or open(stamp).read() != _rel_hash(srcs + _rt_headers(),
+                                                                      " ".join(_host_cmd(srcs, target))):
         return "sources changed"
     return None
+
+
+def _host_cmd(srcs: List[str], target: str) -> List[str]:
+    return [CXX, "-O3", "-std=c++17", "-fPIC", "-shared", "-fopenmp", "-I", os.path.join(CSRC, "include"),
+            *srcs, "-lz", "-o", target]
 
 
 def build_host(force: bool = False, verbose: bool = False) -> str:
@@ -384,16 +396,17 @@ def build_host(force: bool = False, verbose: bool = False) -> str:
     srcs = sorted(os.path.join(rdir, f) for f in os.listdir(rdir) if f.endswith(".cpp"))
     target = os.path.join(LIB, "libtclb_host.so")
     os.makedirs(LIB, exist_ok=True)
-    cmd = [CXX, "-O3", "-std=c++17", "-fPIC", "-shared", "-fopenmp", "-I", os.path.join(CSRC, "include"),
-           *srcs, "-lz", "-o", target + ".tmp"]
-    h = _hash_inputs(srcs + _rt_headers(), " ".join(cmd))
+    cmd = _host_cmd(srcs, target)
+    h = _rel_hash(srcs + _rt_headers(), " ".join(cmd))
     stamp = target + ".hash"
     if not force and os.path.exists(target) and os.path.exists(stamp) and open(stamp).read() == h:
         return target
-    r = subprocess.run(cmd, capture_output=True, text=True)
+    # a per-process temporary: ranks started together may build at once (atomic rename)
+    tmp = f"{target}.{os.getpid()}.tmp"
+    r = subprocess.run(cmd[:-1] + [tmp], capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"host library build failed:\n{r.stderr[-10000:]}")
-    os.replace(target + ".tmp", target)
+    os.replace(tmp, target)
     with open(stamp, "w") as f:
         f.write(h)
     if verbose:
@@ -455,7 +468,7 @@ def build_device_runtime(force: bool = False, verbose: bool = False) -> Optional
     target = os.path.join(LIB, "libtclb_device.so")
     os.makedirs(LIB, exist_ok=True)
     cmd = _device_cmd(srcs)
-    h = _hash_inputs(srcs + _rt_headers(), " ".join(cmd))
+    h = _rel_hash(srcs + _rt_headers(), " ".join(cmd))
     stamp = target + ".hash"
     if not force and os.path.exists(target) and os.path.exists(stamp) and open(stamp).read() == h:
         return target
@@ -480,7 +493,7 @@ def device_runtime_stale() -> Optional[str]:
     if not os.path.exists(target):
         return "missing"
     stamp = target + ".hash"
-    if not os.path.exists(stamp) or open(stamp).read() != _hash_inputs(srcs + _rt_headers(), " ".join(cmd)):
+    if not os.path.exists(stamp) or open(stamp).read() != _rel_hash(srcs + _rt_headers(), " ".join(cmd)):
         return "sources changed"
     return None
 

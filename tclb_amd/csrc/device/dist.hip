@@ -1,6 +1,7 @@
-// GPU side of the native multi-rank loop (tclb_rt/dist_loop.hpp): a context owning this
-// rank's RCCL communicator, a high-priority comm stream and two events, and the
-// transports of dist_iterate:
+// GPU side of the native action loop (tclb_rt/dist_loop.hpp): a context owning this
+// rank's RCCL communicator, a high-priority comm stream and two events, the services of
+// action_loop (stage launches, copy-back of out-of-place stages, the zonal time series,
+// the particle hooks, the grid's packed y rows) and its transports:
 //   * RCCL   — grouped ncclSend/ncclRecv of field planes straight from / into the output
 //              snapshot on the comm stream (xGMI peer-to-peer between the GPUs of a node);
 //              with one rank the peer is this rank itself (self send/receive), which runs
@@ -16,6 +17,8 @@
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <string.h>
+
+#include <chrono>
 
 #include "tclb_rt/dist_loop.hpp"
 
@@ -35,6 +38,8 @@ typedef int (*fn_recv)(void*, size_t, int, int, Comm, hipStream_t);
 typedef int (*fn_group)();
 typedef const char* (*fn_error_string)(int);
 typedef int (*fn_async_error)(Comm, int*);
+typedef int (*fn_all_reduce)(const void*, void*, size_t, int, int, Comm, hipStream_t);
+typedef int (*fn_comm_abort)(Comm);
 
 struct Rccl {
   void* h = nullptr;
@@ -46,6 +51,8 @@ struct Rccl {
   fn_group group_start = nullptr, group_end = nullptr;
   fn_error_string error_string = nullptr;
   fn_async_error async_error = nullptr;
+  fn_all_reduce all_reduce = nullptr;
+  fn_comm_abort comm_abort = nullptr;
 };
 
 char g_err[512];
@@ -73,6 +80,8 @@ int load_rccl(const char* path, Rccl& R) {
   SYM(group_end, "ncclGroupEnd")
   SYM(error_string, "ncclGetErrorString")
   SYM(async_error, "ncclCommGetAsyncError")
+  SYM(all_reduce, "ncclAllReduce")
+  SYM(comm_abort, "ncclCommAbort")
 #undef SYM
   return 0;
 }
@@ -98,39 +107,185 @@ int hip_check(hipError_t e, const char* what) {
   return 2000 + (int)e;
 }
 
-// one stage's exchange: ordered after the work already on the compute stream ks, on the
-// comm stream; finish() orders the compute stream after it
-struct GpuX {
+// pack (unpack = 0) or unpack one block of the grid's y phase: [field][z][y][x] between
+// the snapshot and staging + boff; one thread per element
+template <class T>
+__global__ void __launch_bounds__(256) k_pack(T* snap, T* stg, long long fs, long long sz, long long sy, int px,
+                                              int nfield, int ny, int nz, int y0, int z0, int f0, int unpack) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long long per = (long long)px * ny * nz;
+  if (i >= per * nfield) return;
+  const int f = (int)(i / per);
+  long long r = i - f * per;
+  const int z = (int)(r / ((long long)px * ny));
+  r -= (long long)z * px * ny;
+  const int y = (int)(r / px), x = (int)(r - (long long)y * px);
+  T* a = snap + (long long)(f0 + f) * fs + (long long)(z0 + z) * sz + (long long)(y0 + y) * sy + x;
+  if (unpack) *a = stg[i];
+  else stg[i] = *a;
+}
+
+// active entries of the zonal time series: zonal[idx] = v[iter % len] (and the slope)
+__global__ void k_series(double* zonal, const tclb::SeriesEntry* E, int n, const double* v, const double* dv,
+                         int iter) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const tclb::SeriesEntry e = E[i];
+  const int k = iter % e.len;
+  zonal[e.idx] = v[e.off + k];
+  if (e.len > 1) zonal[e.dtidx] = dv[e.off + k];
+}
+
+__global__ void __launch_bounds__(256) k_nan0(double* a, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n && isnan(a[i])) a[i] = 0.0;
+}
+
+}  // namespace
+
+extern "C" int tclb_part_build_grid(const double*, int, int*, int, int, int, int, int, void*, long long, void*);
+extern "C" int tclb_part_build_tree(const double*, int, int*, int, double, void*, long long, void*);
+extern "C" int tclb_part_rigid_step(double*, const double*, const double*, const unsigned char*, int, double, double,
+                                    double, int, double, double, double, void*);
+
+namespace {
+
+// The services of tclb::action_loop on the GPU.  Launches and copies go to the compute
+// stream ks; an exchange is ordered after the work already on ks, runs on the comm stream
+// (phase A sends / receives, the grid's y-row packs, phase B, the unpacks) and xfinish
+// makes ks wait for it.
+struct GpuSvc {
   Ctx* c;
   hipStream_t ks;
-  int start(char* base, const tclb::HaloOp* ops, int nops) {
-    int r;
-    if ((r = hip_check(hipEventRecord(c->ready, ks), "hipEventRecord")) != 0) return r;
-    if ((r = hip_check(hipStreamWaitEvent(c->cs, c->ready, 0), "hipStreamWaitEvent")) != 0) return r;
+  int prec;
+  tclb::run_fn runf;
+  tclb::sample_fn samplef;
+  int es;              // bytes per stored element
+  long long fs, sz, sy;
+  int px;
+
+  int run(tclb::Launch& L) { return runf(&L, prec); }
+  int sample(tclb::Launch& L, const tclb::SamplePlan& P) { return samplef ? samplef(&L, prec, &P) : 0; }
+
+  int copy_runs(void* dst, const void* src, const tclb::LoopPlan& P, const tclb::StagePlan& st) {
+    for (int i = 0; i < st.nruns; i++) {
+      const int r0 = P.runs[2 * (st.run0 + i)], r1 = P.runs[2 * (st.run0 + i) + 1];
+      const long long off = (long long)r0 * P.fs_bytes, b = (long long)(r1 - r0) * P.fs_bytes;
+      const int r = hip_check(hipMemcpyAsync((char*)dst + off, (const char*)src + off, (size_t)b,
+                                             hipMemcpyDeviceToDevice, ks), "hipMemcpyAsync");
+      if (r != 0) return r;
+    }
+    return 0;
+  }
+
+  int p2p(char* base, char* stg, const tclb::HaloOp* ops, int nops) {
+    if (nops == 0) return 0;
     if (c->transport == 1) {
+      int r;
       if ((r = rccl_check(c, c->R.group_start(), "ncclGroupStart")) != 0) return r;
       for (int i = 0; i < nops; i++) {
         const tclb::HaloOp& o = ops[i];
-        const int e = o.kind == 0 ? c->R.send(base + o.off, (size_t)o.bytes, 0, o.peer, c->comm, c->cs)
-                                  : c->R.recv(base + o.off, (size_t)o.bytes, 0, o.peer, c->comm, c->cs);
+        char* a = (o.buf ? stg : base) + o.off;
+        const int e = o.kind == 0 ? c->R.send(a, (size_t)o.bytes, 0, o.peer, c->comm, c->cs)
+                                  : c->R.recv(a, (size_t)o.bytes, 0, o.peer, c->comm, c->cs);
         if (e != 0) {
           c->R.group_end();
           return rccl_check(c, e, o.kind == 0 ? "ncclSend" : "ncclRecv");
         }
       }
-      if ((r = rccl_check(c, c->R.group_end(), "ncclGroupEnd")) != 0) return r;
-    } else {
-      r = tclb::dist_self_pairs(base, ops, nops, c->rank, [&](char* d, const char* s, long long b) {
-        return hip_check(hipMemcpyAsync(d, s, (size_t)b, hipMemcpyDeviceToDevice, c->cs), "hipMemcpyAsync");
-      });
-      if (r != 0) {
-        if (r == -3) set_err("halo plan", "sends and receives to self do not pair up");
-        return r;
-      }
+      return rccl_check(c, c->R.group_end(), "ncclGroupEnd");
+    }
+    const int r = tclb::dist_self_pairs(base, stg, ops, nops, c->rank, [&](char* d, const char* s, long long b) {
+      return hip_check(hipMemcpyAsync(d, s, (size_t)b, hipMemcpyDeviceToDevice, c->cs), "hipMemcpyAsync");
+    });
+    if (r == -3) set_err("halo plan", "sends and receives to self do not pair up");
+    return r;
+  }
+
+  int packs(char* base, char* stg, const tclb::PackOp* pk, int n, int unpack) {
+    for (int i = 0; i < n; i++) {
+      const tclb::PackOp& o = pk[i];
+      if (o.unpack != unpack) continue;
+      const long long tot = (long long)o.nfield * o.nz * o.ny * px;
+      const unsigned blocks = (unsigned)((tot + 255) / 256);
+      if (es == 8)
+        k_pack<double><<<blocks, 256, 0, c->cs>>>((double*)base, (double*)(stg + o.boff), fs, sz, sy, px, o.nfield,
+                                                  o.ny, o.nz, o.y0, o.z0, o.field0, unpack);
+      else if (es == 4)
+        k_pack<float><<<blocks, 256, 0, c->cs>>>((float*)base, (float*)(stg + o.boff), fs, sz, sy, px, o.nfield,
+                                                 o.ny, o.nz, o.y0, o.z0, o.field0, unpack);
+      else
+        k_pack<unsigned short><<<blocks, 256, 0, c->cs>>>((unsigned short*)base, (unsigned short*)(stg + o.boff), fs,
+                                                          sz, sy, px, o.nfield, o.ny, o.nz, o.y0, o.z0, o.field0,
+                                                          unpack);
+      const int r = hip_check(hipGetLastError(), "k_pack");
+      if (r != 0) return r;
+    }
+    return 0;
+  }
+
+  int xstart(char* base, const tclb::LoopPlan& P, const tclb::StagePlan& st) {
+    int r;
+    char* stg = (char*)P.staging;
+    if ((r = hip_check(hipEventRecord(c->ready, ks), "hipEventRecord")) != 0) return r;
+    if ((r = hip_check(hipStreamWaitEvent(c->cs, c->ready, 0), "hipStreamWaitEvent")) != 0) return r;
+    if ((r = p2p(base, stg, P.ops + st.op0, st.nops)) != 0) return r;
+    if (st.nopsb > 0) {
+      if ((r = packs(base, stg, P.packs + st.pk0, st.npk, 0)) != 0) return r;
+      if ((r = p2p(base, stg, P.ops + st.opb0, st.nopsb)) != 0) return r;
+      if ((r = packs(base, stg, P.packs + st.pk0, st.npk, 1)) != 0) return r;
     }
     return hip_check(hipEventRecord(c->done, c->cs), "hipEventRecord");
   }
-  int finish() { return hip_check(hipStreamWaitEvent(ks, c->done, 0), "hipStreamWaitEvent"); }
+  int xfinish() { return hip_check(hipStreamWaitEvent(ks, c->done, 0), "hipStreamWaitEvent"); }
+
+  int series(const tclb::LoopPlan& P, int iter) {
+    k_series<<<(P.nseries + 63) / 64, 64, 0, ks>>>(P.zonal, P.series, P.nseries, P.svals, P.sslopes, iter);
+    return hip_check(hipGetLastError(), "k_series");
+  }
+
+  int part_pre(tclb::Launch& L, const tclb::LoopPlan& P) {
+    const tclb::PartPlan& q = *P.part;
+    int r = hip_check(hipMemsetAsync(q.acc, 0, sizeof(double) * 6 * (size_t)(q.n > 0 ? q.n : 1), ks), "memset");
+    if (r != 0) return r;
+    if (q.container == 1) r = tclb_part_build_grid(q.P, q.n, q.grid, q.gdim[0], q.gdim[1], q.gdim[2], q.cell, q.ncell,
+                                                   q.tmp, q.tmp_bytes, ks);
+    else if (q.container == 2) r = tclb_part_build_tree(q.P, q.n, q.grid, q.nl, q.mscale, q.tmp, q.tmp_bytes, ks);
+    if (r != 0) {
+      set_err("solid container build", hipGetErrorString((hipError_t)(r > 0 ? r : 1)));
+      return 3000 + (r < 0 ? -r : r);
+    }
+    L.ext[2] = q.P;
+    L.ext[3] = q.acc;
+    L.next[2] = q.n;
+    L.ext[4] = q.container ? q.grid : nullptr;
+    L.next[4] = q.container ? q.grid_n : 0;
+    return 0;
+  }
+
+  int part_post(tclb::Launch& L, const tclb::LoopPlan& P, int step) {
+    const tclb::PartPlan& q = *P.part;
+    int r;
+    const int na = 6 * q.n;
+    if (q.allreduce && c->transport == 1 && c->nranks > 1 && na > 0) {
+      // ncclFloat64 = 8, ncclSum = 0; on the compute stream, after the stage's kernels
+      if ((r = rccl_check(c, c->R.all_reduce(q.acc, q.acc, (size_t)na, 8, 0, c->comm, ks), "ncclAllReduce")) != 0)
+        return r;
+    }
+    if (na > 0) {
+      k_nan0<<<(na + 255) / 256, 256, 0, ks>>>(q.acc, na);
+      if ((r = hip_check(hipGetLastError(), "k_nan0")) != 0) return r;
+    }
+    L.next[2] = 0;
+    L.ext[4] = nullptr;
+    L.next[4] = 0;
+    if (step && q.integrate && q.n > 0) {
+      r = tclb_part_rigid_step(q.P, q.acc, q.m, q.free_, q.n, q.a[0], q.a[1], q.a[2], q.periodic, q.period[0],
+                               q.period[1], q.period[2], ks);
+      if (r != 0) return hip_check((hipError_t)r, "rigid step");
+    }
+    return 0;
+  }
 };
 
 }  // namespace
@@ -191,38 +346,86 @@ void* tclb_dist_ctx_create(const char* rccl_path, int transport, int nranks, int
 void tclb_dist_ctx_destroy(void* ctx) {
   Ctx* c = (Ctx*)ctx;
   if (!c) return;
-  if (c->cs) hipStreamSynchronize(c->cs);
+  if (c->cs) (void)hipStreamSynchronize(c->cs);
   if (c->comm) c->R.comm_destroy(c->comm);
-  if (c->ready) hipEventDestroy(c->ready);
-  if (c->done) hipEventDestroy(c->done);
-  if (c->cs) hipStreamDestroy(c->cs);
+  if (c->ready) (void)hipEventDestroy(c->ready);
+  if (c->done) (void)hipEventDestroy(c->done);
+  if (c->cs) (void)hipStreamDestroy(c->cs);
   delete c;
 }
 
-// the n steps of an action (tclb_rt/dist_loop.hpp); run / sample are the model library's
-// tclb_<model>_run / tclb_<model>_sample; launches go to L->stream
-int tclb_dist_iterate(void* ctx, const tclb::Launch* L, int prec, int nsteps, int glob_last,
-                      const tclb::DistPlan* P, tclb::run_fn run, tclb::sample_fn sample,
-                      const tclb::SamplePlan* sp) {
+// the n steps of an action (tclb_rt/dist_loop.hpp action_loop); run / sample are the
+// model library's tclb_<model>_run / tclb_<model>_sample; launches go to L->stream.
+// es: bytes per stored element (the grid's pack kernels)
+int tclb_loop_iterate(void* ctx, const tclb::Launch* L, int prec, int es, int nsteps, int glob_last, int init,
+                      const tclb::LoopPlan* P, tclb::run_fn run, tclb::sample_fn sample) {
   Ctx* c = (Ctx*)ctx;
-  GpuX x{c, (hipStream_t)L->stream};
-  int r = tclb::dist_iterate(*L, prec, nsteps, glob_last, *P, x, run, sample, sp);
-  if (r == 0 && c->transport == 1) {
-    int ae = 0;
-    if (c->R.async_error(c->comm, &ae) == 0 && ae != 0) r = rccl_check(c, ae, "RCCL async error");
-  }
-  return r;
+  GpuSvc sv{c, (hipStream_t)L->stream, prec, run, sample, es, L->fs, L->sz, L->sy, L->px};
+  return tclb::action_loop(sv, *L, nsteps, glob_last, *P, init);
 }
 
 // one exchange outside the loop (the Python step path of the same plan)
 int tclb_dist_exchange(void* ctx, void* base, const tclb::HaloOp* ops, int nops, void* stream) {
   Ctx* c = (Ctx*)ctx;
-  GpuX x{c, (hipStream_t)stream};
-  int r = x.start((char*)base, ops, nops);
-  return r != 0 ? r : x.finish();
+  GpuSvc sv{c, (hipStream_t)stream, 0, nullptr, nullptr, 8, 0, 0, 0, 0};
+  tclb::LoopPlan P = {};
+  tclb::StagePlan st = {};
+  P.ops = ops;
+  st.nops = nops;
+  int r = sv.xstart((char*)base, P, st);
+  return r != 0 ? r : sv.xfinish();
 }
 
-int tclb_dist_sizeof_plan() { return (int)sizeof(tclb::DistPlan); }
+// wait for the work queued on `stream` with the communicator watched: polls the RCCL
+// asynchronous error while the stream runs and aborts the communicator on an error or
+// after timeout_ms (a dead peer then ends this rank's wait instead of hanging it)
+int tclb_dist_wait(void* ctx, void* stream, int timeout_ms) {
+  Ctx* c = (Ctx*)ctx;
+  hipEvent_t e;
+  int r = hip_check(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
+  if (r != 0) return r;
+  if ((r = hip_check(hipEventRecord(e, (hipStream_t)stream), "hipEventRecord")) != 0) {
+    (void)hipEventDestroy(e);
+    return r;
+  }
+  const auto t0 = std::chrono::steady_clock::now();
+  long long spins = 0;
+  for (;;) {
+    const hipError_t q = hipEventQuery(e);
+    if (q == hipSuccess) break;
+    if (q != hipErrorNotReady) {
+      r = hip_check(q, "hipEventQuery");
+      break;
+    }
+    if (c->transport == 1 && c->comm) {
+      int ae = 0;
+      if (c->R.async_error(c->comm, &ae) == 0 && ae != 0) {
+        r = rccl_check(c, ae, "RCCL async error");
+        c->R.comm_abort(c->comm);
+        c->comm = nullptr;
+        break;
+      }
+    }
+    if (timeout_ms > 0 && (++spins & 1023) == 0 &&
+        std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count() > timeout_ms) {
+      set_err("tclb_dist_wait", "timed out: aborting the communicator");
+      if (c->transport == 1 && c->comm) {
+        c->R.comm_abort(c->comm);
+        c->comm = nullptr;
+      }
+      r = -110;
+      break;
+    }
+  }
+  (void)hipEventDestroy(e);
+  return r;
+}
+
+int tclb_loop_sizeof_plan() { return (int)sizeof(tclb::LoopPlan); }
+int tclb_loop_sizeof_stage() { return (int)sizeof(tclb::StagePlan); }
+int tclb_loop_sizeof_part() { return (int)sizeof(tclb::PartPlan); }
+int tclb_loop_sizeof_pack() { return (int)sizeof(tclb::PackOp); }
+int tclb_loop_sizeof_series() { return (int)sizeof(tclb::SeriesEntry); }
 int tclb_dist_sizeof_op() { return (int)sizeof(tclb::HaloOp); }
 
 }  // extern "C"

@@ -1,0 +1,107 @@
+// Snapshot allocator: the A/B population buffers are the only large allocations of a
+// lattice (2 x 29 GB for d3q27 fp64 512^3), and where they land in HBM decides how fast
+// the collide-stream kernel reads them (tools/direction_probe.py: the same kernel runs
+// 9.7 ms or 11.8 ms per dispatch depending on the placement of the buffer it reads).
+// The reference pre-allocates every snapshot in one cudaMalloc (src/cross.cu:52-117,
+// cudaPreAlloc / cudaAllocFinalize); here the placement is a choice:
+//
+//   mode 0  hipMalloc                                   (what the torch allocator does)
+//   mode 1  hipExtMallocWithFlags(hipDeviceMallocContiguous): one physically contiguous
+//           range, so the GPU page tables can use their largest fragments
+//   mode 2  virtual memory API: hipMemCreate of the whole size at the recommended
+//           granularity, mapped into a range reserved at a 1 GiB-aligned address
+//
+// Each call returns 0 or a HIP error code; tclb_snap_free releases by the same mode.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <map>
+#include <mutex>
+
+namespace {
+
+struct VmmRange {
+  hipMemGenericAllocationHandle_t handle;
+  size_t size;
+};
+
+std::mutex g_mu;
+std::map<uintptr_t, VmmRange> g_vmm;
+
+int vmm_alloc(void** out, size_t bytes, int device) {
+  hipMemAllocationProp prop = {};
+  prop.type = hipMemAllocationTypePinned;
+  prop.location.type = hipMemLocationTypeDevice;
+  prop.location.id = device;
+  size_t gran = 0;
+  hipError_t e = hipMemGetAllocationGranularity(&gran, &prop, hipMemAllocationGranularityRecommended);
+  if (e != hipSuccess) return (int)e;
+  if (gran == 0) gran = 2u << 20;
+  const size_t size = (bytes + gran - 1) / gran * gran;
+  hipMemGenericAllocationHandle_t h;
+  if ((e = hipMemCreate(&h, size, &prop, 0)) != hipSuccess) return (int)e;
+  void* p = nullptr;
+  const size_t align = size_t(1) << 30;
+  if ((e = hipMemAddressReserve(&p, size, align, nullptr, 0)) != hipSuccess) {
+    hipMemRelease(h);
+    return (int)e;
+  }
+  if ((e = hipMemMap(p, size, 0, h, 0)) != hipSuccess) {
+    hipMemAddressFree(p, size);
+    hipMemRelease(h);
+    return (int)e;
+  }
+  hipMemAccessDesc acc = {};
+  acc.location = prop.location;
+  acc.flags = hipMemAccessFlagsProtReadWrite;
+  if ((e = hipMemSetAccess(p, size, &acc, 1)) != hipSuccess) {
+    hipMemUnmap(p, size);
+    hipMemAddressFree(p, size);
+    hipMemRelease(h);
+    return (int)e;
+  }
+  std::lock_guard<std::mutex> lk(g_mu);
+  g_vmm[(uintptr_t)p] = VmmRange{h, size};
+  *out = p;
+  return 0;
+}
+
+int vmm_free(void* p) {
+  VmmRange r;
+  {
+    std::lock_guard<std::mutex> lk(g_mu);
+    auto it = g_vmm.find((uintptr_t)p);
+    if (it == g_vmm.end()) return (int)hipErrorInvalidValue;
+    r = it->second;
+    g_vmm.erase(it);
+  }
+  hipError_t e = hipMemUnmap(p, r.size);
+  if (e == hipSuccess) e = hipMemAddressFree(p, r.size);
+  if (e == hipSuccess) e = hipMemRelease(r.handle);
+  return (int)e;
+}
+
+}  // namespace
+
+extern "C" int tclb_snap_alloc(void** out, size_t bytes, int mode, int device) {
+  if (!out || bytes == 0) return (int)hipErrorInvalidValue;
+  *out = nullptr;
+  hipError_t e = hipSetDevice(device);
+  if (e != hipSuccess) return (int)e;
+  switch (mode) {
+    case 0: e = hipMalloc(out, bytes); break;
+    case 1: e = hipExtMallocWithFlags(out, bytes, hipDeviceMallocContiguous); break;
+    case 2: return vmm_alloc(out, bytes, device);
+    default: return (int)hipErrorInvalidValue;
+  }
+  return (int)e;
+}
+
+extern "C" int tclb_snap_free(void* p, int mode) {
+  if (!p) return 0;
+  // the buffer may still be read or written by queued kernels of any stream
+  hipError_t e = hipDeviceSynchronize();
+  if (e != hipSuccess) return (int)e;
+  if (mode == 2) return vmm_free(p);
+  return (int)hipFree(p);
+}

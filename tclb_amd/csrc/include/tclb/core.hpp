@@ -94,6 +94,10 @@ struct Launch {
   long long mfs, msy, msz;
   int moy, moz;
   signed char mslot[TCLB_MIRROR_FIELDS];
+  // Tile windows (GPU): log2 of the number of contiguous tile ranges the work-groups are
+  // dealt over (executor_hip.hpp tile_id); 0 = the hardware's linear block order
+  int tile_split;
+  int reserved3;
 };
 
 // Zonal-table read (reference ZoneSettings, one value per zone): the zone comes from the

@@ -103,31 +103,35 @@ __device__ __forceinline__ void block_globals_flush(const R* acc, double* dst) {
   }
 }
 
-// Block -> tile map.  Workgroups are dealt round-robin over the 8 XCDs (b and b+8 share
-// an L2; MI355X_MICROARCH.md, Workgroup dispatch).  With TCLB_XCD_REMAP the linear block
-// id b is remapped so that XCD (b % 8) owns one contiguous 1/8 of the tiles (a z-range):
-// x-neighbouring tiles, which share the partial 128-B lines of the x-shifted pull loads,
-// and y/z-neighbouring tiles of stencil stages then meet in the same L2.  Speed only:
-// any placement gives the same result.
-#ifndef TCLB_XCD_REMAP
-#define TCLB_XCD_REMAP 0
-#endif
-__device__ __forceinline__ uint3 tile_id() {
-#if TCLB_XCD_REMAP
-  const unsigned gx = gridDim.x, gy = gridDim.y, T = gridDim.x * gridDim.y * gridDim.z;
-  unsigned b = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
-  if ((T & 7u) == 0u) b = (b & 7u) * (T >> 3) + (b >> 3);
+// Block -> tile map.  The hardware deals work-groups round-robin over the 8 XCDs (b and
+// b+8 share an L2; MI355X_MICROARCH.md, Workgroup dispatch) and in linear order in time,
+// so with the identity map every resident wave of the chip works in ONE narrow window of
+// the lattice: 27 read + 27 written field planes, each 2^k bytes apart, hit the HBM
+// channels and banks at the same offsets at once, and the speed of a dispatch then depends
+// on where the snapshot pages landed (tools/direction_probe.py: 9.5-11.8 ms per d3q27
+// fp64 512^3 step from one allocation to the next, the same kernel).  With
+// L.tile_split = k > 0 the linear block id b is remapped so that block b works in window
+// (b mod 2^k), one of 2^k contiguous tile ranges (z-ranges): 2^k x 54 streams spread over
+// the lattice, and with 2^k = 8 each XCD owns one window, so x-neighbouring tiles (which
+// share the partial 128-B lines of the x-shifted pulls) and y/z neighbours of stencil
+// stages meet in the same L2.  Speed only: any map gives the same result.
+__device__ __forceinline__ unsigned tile_linear(const Launch& L, unsigned b, unsigned T) {
+  const unsigned k = (unsigned)L.tile_split;
+  if (k > 0u && k < 16u && (T & ((1u << k) - 1u)) == 0u) b = (b & ((1u << k) - 1u)) * (T >> k) + (b >> k);
+  return b;
+}
+__device__ __forceinline__ uint3 tile_id(const Launch& L) {
+  const unsigned gx = gridDim.x, gy = gridDim.y;
+  if (L.tile_split <= 0) return make_uint3(blockIdx.x, blockIdx.y, blockIdx.z);
+  const unsigned b = tile_linear(L, blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z), gx * gy * gridDim.z);
   return make_uint3(b % gx, (b / gx) % gy, b / (gx * gy));
-#else
-  return make_uint3(blockIdx.x, blockIdx.y, blockIdx.z);
-#endif
 }
 
 template <class Model, class R, class S, int STG, bool GLOB>
 __device__ __forceinline__ void stage_body(const Launch& L) {
   typedef typename Model::template NodeT<R, S, GLOB> N;
   typedef typename N::G_ G;   // fp64 accumulators, also in fp32-compute builds (core.hpp glob_acc)
-  const uint3 t = tile_id();
+  const uint3 t = tile_id(L);
   const int x = L.xlo + (int)(t.x * blockDim.x + threadIdx.x);
   // blockDim.x is a multiple of 64 (launch_shape), so a wave covers 64 x of one row:
   // y is wave-uniform.  In the row-form instantiations (N::ROWA_, the globals kernels)

@@ -36,10 +36,11 @@ __global__ void __launch_bounds__(TILE_BX * TILE_BY) k_tile(const Launch L) {
   constexpr int NL = (PLANE + NTH - 1) / NTH;   // plane elements per thread
   __shared__ S tile[NT * SLOT];
   const int tx = threadIdx.x, ty = threadIdx.y, tid = tx + TILE_BX * ty;
-  const int x0 = L.xlo + (int)blockIdx.x * TILE_BX;
-  const int y0 = L.ylo + (int)blockIdx.y * TILE_BY;
+  const uint3 tb = tile_id(L);     // executor_hip.hpp: the block -> tile window map
+  const int x0 = L.xlo + (int)tb.x * TILE_BX;
+  const int y0 = L.ylo + (int)tb.y * TILE_BY;
   constexpr int ZC = Model::tile_zc(STG);
-  const int zb = L.zlo + (int)blockIdx.z * ZC;
+  const int zb = L.zlo + (int)tb.z * ZC;
   const int ze = zb + ZC < L.zhi ? zb + ZC : L.zhi;
   const int x = x0 + tx;
   const int y = __builtin_amdgcn_readfirstlane(y0 + ty);   // a wave is one row of the tile

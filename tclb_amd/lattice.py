@@ -30,7 +30,7 @@ from .models.dsl import Model
 from .ops import abi
 from .parallel.comm import Comm, LoopbackComm
 from .parallel.decomp import Slab, decompose
-from .parallel.native import NativeDist, native_dist_enabled
+from .parallel.native import NativeLoop, native_dist_enabled
 from .utils import trace
 
 _SAFE_MATH = {k: getattr(math, k) for k in ("sqrt", "exp", "log", "sin", "cos", "tan", "atan", "atan2", "pi",
@@ -163,11 +163,14 @@ class Lattice:
                           for a in ((1, 2) if ax == 3 else (ax,))}
         self.halo_lo, self.halo_hi = self.halo_sets[2 if ax == 3 else ax]
         self._halo_bufs = {}
-        self._dist = None                 # NativeDist of the native multi-rank loop (lazy)
+        self._dist = None                 # NativeLoop of the native action loop (parallel/native.py)
         # native multi-step loop (ops.abi ModelLib.iterate) for halo-free lattices
         self.native_loop = (os.environ.get("TCLB_NATIVE_LOOP", "1") != "0") if native_loop is None else native_loop
         for s in m.settings:
             self.set_setting(s.name, s.default, _init=True)
+        # GPU block -> tile windows (executor_hip.hpp tile_id): log2 of the number of
+        # contiguous tile ranges the work-groups are dealt over; env TCLB_TILE_SPLIT
+        self.tile_split = self._default_tile_split()
         self._L = self._base_launch()
         self.callbacks = []
         self.samplers = []        # tclb_amd.sampler.Sampler: probes recorded every iteration
@@ -176,6 +179,22 @@ class Lattice:
         self.cuts = None
         self.particles = None     # ParticleSystem with pre_stage/post_stage/step hooks
         self.average_start = 0
+        # the native loop of a multi-rank lattice is created with the lattice, so its
+        # collective set-up (the RCCL communicator) happens at the same point on every rank
+        if (self.comm.distributed and self.native_loop and native_dist_enabled() and self.lib.has_iterate
+                and NativeLoop.supported(self)):
+            self._dist = NativeLoop(self)
+
+    def _default_tile_split(self) -> int:
+        env = os.environ.get("TCLB_TILE_SPLIT")
+        if env is not None and env != "":
+            return max(0, min(15, int(env)))
+        return 0
+
+    def set_tile_split(self, k: int):
+        """log2 of the tile windows of the GPU kernels (0: linear block order)"""
+        self.tile_split = max(0, min(15, int(k)))
+        self._L.tile_split = self.tile_split
 
     def new_snapshot(self, uninit: bool = False) -> torch.Tensor:
         """a zeroed snapshot buffer with the layout of snaps[0/1] ([nf][NZ][NY][px], field
@@ -211,6 +230,7 @@ class Lattice:
         L.block_x, L.block_y = self.block
         L.flags = self.flags.data_ptr()
         L.storage_shift = 1 if self.storage_shift else 0
+        L.tile_split = self.tile_split
         return L
 
     def _sync_settings(self):
@@ -600,38 +620,63 @@ class Lattice:
             self.globals[gl.name] = float(vals[i])
 
     def init(self):
-        """Action Init (reference: Lattice::Init -> Action_Init, src/Lattice.cu.Rt:799-821)."""
+        """Action Init (reference: Lattice::Init -> Action_Init, src/Lattice.cu.Rt:799-821):
+        through the native action loop when it takes the action (e.g. d2q9_csf's
+        fixed-point wall-normal stage), else the Python step path."""
         self.iter = 0
-        self.run_action("Init", glob=False)
+        if self._native_path("Init") == "loop":
+            self.iterate(1, glob_last=False, action="Init")
+            self.iter = 0
+        else:
+            self.run_action("Init", glob=False)
+
+    def _native_path(self, action: str) -> Optional[str]:
+        """how `action` steps: "lib" — one call into the model library (one rank, no
+        ghosts, plain stages: tclb::iterate_action); "loop" — the native action loop
+        (parallel/native.py, tclb_rt/dist_loop.hpp: any rank count, slab or Y x Z grid,
+        particle / out-of-place / fixed-point stages, time series, samplers); None — the
+        Python step path (per-step callbacks, a particle system that talks to another
+        program, TCLB_NATIVE_LOOP=0)"""
+        if not (self.native_loop and self.lib.has_iterate):
+            return None
+        act = self.model.action(action)
+        if act is None or self.callbacks:
+            return None
+        if self.particles is not None and not self.particles.native_ok():
+            return None
+        if self.comm.distributed and not native_dist_enabled():
+            return None
+        if not NativeLoop.supported(self):
+            return None
+        special = any(self.model.stage(s).fixed_point or self.model.stage(s).particle or
+                      self.model.stage(s).snapshot_reads for s in act.stages)
+        if (self.g == 0 and not self.comm.distributed and not self.zseries and self.particles is None
+                and len(self.samplers) <= 1 and not special):
+            return "lib"
+        return "loop"
 
     def _native_ok(self, action: str) -> bool:
-        if not (self.native_loop and self.lib.has_iterate):
-            return False
-        if self.comm.distributed:
-            # slab-split ranks: the native multi-rank loop (parallel/native.py)
-            if not (native_dist_enabled() and NativeDist.supported(self)):
-                return False
-        elif self.g != 0:
-            return False
-        if self.zseries or self.callbacks or self.particles is not None or len(self.samplers) > 1:
-            return False
-        act = self.model.action(action)
-        return act is not None and not any(self.model.stage(s).fixed_point or self.model.stage(s).particle or
-                                           self.model.stage(s).snapshot_reads for s in act.stages)
+        return self._native_path(action) is not None
 
     def iterate(self, n: int, glob_last: bool = True, action: str = "Iteration", reduce: bool = True):
         """Reference Lattice::Iterate (src/Lattice.cu.Rt:900-989): globals on the last step.
 
-        Without time series, callbacks or particles the n steps run in one native call: on
-        one rank tclb::iterate_action (one kernel launch per stage, no Python per step), on
-        slab-split ranks the multi-rank loop of parallel/native.py (border launches, RCCL
-        exchange into the ghost planes, interior launch)."""
+        The n steps run in one native call whenever nothing needs Python between steps:
+        on one rank without ghosts and with plain stages tclb::iterate_action of the model
+        library (one kernel launch per stage); otherwise the native action loop of
+        parallel/native.py (border launches, RCCL exchange into the ghost planes, interior
+        launch; particle hooks, out-of-place and fixed-point stages, time series,
+        samplers)."""
         if n <= 0:
             return
-        if self._native_ok(action):
+        path = self._native_path(action)
+        if path is not None:
             m = self.model
             stages = [m.stage_index(s) for s in m.action(action).stages]
             self._sync_settings()
+            if self.zseries and any(self.zsettings[k[0]].endswith("InObj") for k in self.zseries):
+                # an Objective weight follows a series: keep the weighted sum on
+                self._glob_flags &= ~4
             if glob_last:
                 self.globals_t.zero_()
             L = self._L
@@ -642,23 +687,33 @@ class Lattice:
             L.iter = self.iter
             L.reserved1 = self.iter - self.average_start + 1
             L.stream = self._stream()
-            L.glob = self._glob_flags            # bit 0 set per step by iterate_action
-            smp = self.samplers[0] if self.samplers else None
+            L.glob = self._glob_flags            # bit 0 set per step by the loop
             with trace.span(f"iterate {action} x{n}"):
-                if self.comm.distributed:
-                    if self._dist is None:
-                        self._dist = NativeDist(self)
-                    self._dist.iterate(L, self.prec, n, stages, glob_last, smp.plan_for(n) if smp else None)
-                else:
+                if path == "lib":
+                    smp = self.samplers[0] if self.samplers else None
                     self.lib.iterate(L, self.prec, n, stages, glob_last, smp.plan_for(n) if smp else None)
+                else:
+                    if self._dist is None:
+                        self._dist = NativeLoop(self)
+                    self._dist.iterate(L, n, action, glob_last)
             if trace.SYNC:
                 trace.after_launch(self, f"{self.model.name} native loop")
-            if smp:
-                smp.advance(n)
+            if action != "Init":
+                for smp in self.samplers:
+                    smp.advance(n)
+            if self.particles is not None:
+                self.particles.after_native(self, n, action)
             self.iter += n
             if n % 2 == 1:
                 self.cur = 1 - self.cur
+            if self.zseries:
+                # the host copy of the zonal table follows the device: entries of the last step
+                self.iter -= 1
+                self.apply_series()
+                self.iter += 1
             if glob_last and reduce:
+                if self._dist is not None:
+                    self._dist.wait()
                 self._reduce_globals()
             return
         for i in range(n):

@@ -443,7 +443,7 @@ class Model:
             if k > 0:
                 reads = set(st.read_fields or [])
                 if st.load_densities and not st.init:
-                    reads |= {d.field.nicename for d in self.densities}
+                    reads |= {d.field.nicename for d in self.densities if self.matches(d.field, st.load_densities)}
                 out |= reads - written
             written |= {f.nicename for f in self.fields if self.matches(f, st.save_fields)}
         return sorted(out)

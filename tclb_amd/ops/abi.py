@@ -69,6 +69,9 @@ class Launch(ctypes.Structure):
         ("moy", ctypes.c_int),
         ("moz", ctypes.c_int),
         ("mslot", ctypes.c_byte * MIRROR_FIELDS),
+        # log2 of the tile windows of the GPU block -> tile map (executor_hip.hpp tile_id)
+        ("tile_split", ctypes.c_int),
+        ("reserved3", ctypes.c_int),
     ]
 
 

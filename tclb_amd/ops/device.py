@@ -24,7 +24,7 @@ def lib():
             path = os.path.join(B.LIB, "libtclb_device.so")
             stale = B.device_runtime_stale()
             if stale is not None:
-                if os.path.exists(B.HIPCC):
+                if os.path.exists(B.HIPCC) and not os.environ.get("TCLB_NO_BUILD"):
                     B.build_device_runtime()
                 else:
                     raise DeviceRuntimeError(f"device runtime library not usable ({stale}): {path}")
@@ -34,6 +34,14 @@ def lib():
             L.tclb_part_nan_to_zero.restype = i
             L.tclb_part_rigid_step.argtypes = [P, P, P, P, i, d, d, d, i, d, d, d, P]
             L.tclb_part_rigid_step.restype = i
+            L.tclb_part_build_grid.argtypes = [P, i, P, i, i, i, i, i, P, ctypes.c_longlong, P]
+            L.tclb_part_build_grid.restype = i
+            L.tclb_part_build_tree.argtypes = [P, i, P, i, d, P, ctypes.c_longlong, P]
+            L.tclb_part_build_tree.restype = i
+            L.tclb_snap_alloc.argtypes = [ctypes.POINTER(P), ctypes.c_size_t, i, i]
+            L.tclb_snap_alloc.restype = i
+            L.tclb_snap_free.argtypes = [P, i]
+            L.tclb_snap_free.restype = i
             _lib = L
     return _lib
 
@@ -53,3 +61,36 @@ def rigid_step(P, acc, m, free, n: int, a, periodic: int, period, stream: int):
                                       float(a[0]), float(a[1]), float(a[2]), periodic,
                                       float(period[0]), float(period[1]), float(period[2]), stream),
            "particle integration")
+
+
+SNAP_ALLOC_MODES = {"torch": -1, "hip": 0, "contiguous": 1, "vmm": 2}
+
+
+class _SnapBlock:
+    """owner of one tclb_snap_alloc range, exposed through __cuda_array_interface__ (the
+    torch tensor made from it keeps this object alive; the range is freed with it)"""
+
+    def __init__(self, nbytes: int, mode: int, device: int):
+        p = ctypes.c_void_p()
+        _check(lib().tclb_snap_alloc(ctypes.byref(p), nbytes, mode, device), f"snapshot allocation (mode {mode})")
+        self.ptr, self.nbytes, self.mode = p.value, nbytes, mode
+        self.__cuda_array_interface__ = {"shape": (nbytes,), "typestr": "|u1", "data": (self.ptr, False),
+                                         "version": 2, "strides": None}
+
+    def __del__(self):
+        if self.ptr and _lib is not None:
+            _lib.tclb_snap_free(ctypes.c_void_p(self.ptr), self.mode)
+            self.ptr = None
+
+
+def snap_buffer(nbytes: int, mode: str, device):
+    """a uint8 device tensor of nbytes from the native snapshot allocator
+    (csrc/device/snapalloc.hip): mode "hip" (hipMalloc), "contiguous" (one physically
+    contiguous range) or "vmm" (hipMemCreate + a 1 GiB-aligned reservation)"""
+    import torch
+    m = SNAP_ALLOC_MODES[mode]
+    dev = torch.device(device)
+    blk = _SnapBlock(int(nbytes), m, dev.index or 0)
+    t = torch.as_tensor(blk, device=dev)
+    assert t.data_ptr() == blk.ptr and t.numel() == nbytes
+    return t

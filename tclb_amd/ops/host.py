@@ -17,7 +17,10 @@ def lib():
         if _lib is None:
             from .. import build as B
             path = os.path.join(B.LIB, "libtclb_host.so")
-            if B.host_runtime_stale() is not None:
+            stale = B.host_runtime_stale()
+            if stale is not None:
+                if os.environ.get("TCLB_NO_BUILD"):
+                    raise RuntimeError(f"libtclb_host.so not usable ({stale}) and TCLB_NO_BUILD is set: {path}")
                 B.build_host()
             L = ctypes.CDLL(path)
             P = ctypes.c_void_p
@@ -36,6 +39,15 @@ def lib():
             L.tclb_nan_scan_f32.restype = ctypes.c_longlong
             L.tclb_png_write.argtypes = [ctypes.c_char_p, P, i, i]
             L.tclb_png_write.restype = i
+            d = ctypes.c_double
+            L.tclb_part_build_grid_cpu.argtypes = [P, i, P, i, i, i, i, i]
+            L.tclb_part_build_grid_cpu.restype = i
+            L.tclb_part_build_tree_cpu.argtypes = [P, i, P, i, d]
+            L.tclb_part_build_tree_cpu.restype = i
+            L.tclb_part_nan_to_zero_cpu.argtypes = [P, i]
+            L.tclb_part_nan_to_zero_cpu.restype = None
+            L.tclb_part_rigid_step_cpu.argtypes = [P, P, P, P, i, d, d, d, i, d, d, d]
+            L.tclb_part_rigid_step_cpu.restype = None
             _lib = L
     return _lib
 

@@ -1,22 +1,27 @@
-"""Native multi-rank iteration: the n steps of an action of a slab-decomposed lattice run
-in one C++ call (csrc/include/tclb_rt/dist_loop.hpp) — border launches, halo exchange,
-interior launch, per stage and step, with no Python in between.
+"""Native action loop: the n steps of an action run in one C++ call
+(csrc/include/tclb_rt/dist_loop.hpp action_loop) — stage launches with the border /
+exchange / interior split, out-of-place and fixed-point stages, the particle hooks, the
+zonal time series and every sampler, on one rank or many, over a slab or a Y x Z process
+grid, with no Python in between.
 
-Reference: each MPI rank runs Lattice::Iterate in C++, RunBorder -> MPIStream_A ->
-RunInterior -> MPIStream_B (src/Lattice.cu.Rt:466-533,900-989), with received margins
-copied into the next snapshot's margin blocks (src/Lattice.cu.Rt:371-378,439-456).
+Reference: each MPI rank runs Lattice::Iterate in C++: RunBorder -> MPIStream_A ->
+RunInterior -> MPIStream_B (src/Lattice.cu.Rt:466-533,900-989), particle stages with
+CopyInParticles / CopyOutParticles (:392-437), fixed-point stages (:484), the zone index of
+the time series (:473-477), samplers (:1376-1389).
 
 Transports (``TCLB_DIST_TRANSPORT`` = auto | rccl | copy):
 
 * ``rccl``     — GPU: this module's own RCCL communicator (librccl dlopen'ed from torch's
   lib dir; the unique id travels through torch.distributed), grouped ncclSend/ncclRecv of
   each halo field's planes straight from / into the output snapshot on a high-priority
-  comm stream (no pack, no unpack).  With one rank (LoopbackComm) the peer is the rank
+  comm stream (no pack, no unpack; the Y x Z grid's y rows go through a staging buffer),
+  ncclAllReduce of the particle forces.  With one rank (LoopbackComm) the peer is the rank
   itself: RCCL self send/receive, so a single MI355X exercises the multi-GPU code.
-* ``copy``     — one rank as its own neighbour, the plan executed as device-to-device
-  copies (GPU) or memcpy (CPU).
-* ``callback`` — CPU ranks (gloo): the loop calls back into Python per exchange, which
-  runs the plan's ops as torch.distributed isend/irecv.  Same plan, same loop.
+* ``copy``     — one rank as its own neighbour (or no neighbour at all), the plan executed
+  as device-to-device copies (GPU) or memcpy (CPU).
+* ``callback`` — CPU ranks (gloo): the loop calls back into Python per exchange phase and
+  per particle-force all-reduce, which run as torch.distributed operations.  Same plan,
+  same loop.
 """
 from __future__ import annotations
 
@@ -24,8 +29,9 @@ import ctypes
 import os
 import threading
 import traceback
-from typing import Dict, Optional, Tuple
+from typing import Dict, List, Optional, Tuple
 
+import numpy as np
 import torch
 
 from ..ops import abi
@@ -33,23 +39,57 @@ from .comm import LoopbackComm, TorchDistComm
 
 MAX_STAGES = 32       # dist_loop.hpp DIST_MAX_STAGES
 TAG_HI = 1 << 12      # tag offset of the fields read from above
+TAG_Y = 1 << 13       # tag offset of the grid's y phase
+FIXED_POINT_SWEEPS = 100
 
 
 class HaloOp(ctypes.Structure):
     _fields_ = [("off", ctypes.c_longlong), ("bytes", ctypes.c_longlong), ("kind", ctypes.c_int),
-                ("peer", ctypes.c_int), ("tag", ctypes.c_int), ("reserved", ctypes.c_int)]
+                ("peer", ctypes.c_int), ("tag", ctypes.c_int), ("buf", ctypes.c_int)]
 
 
-class DistPlan(ctypes.Structure):
-    _fields_ = [("axis", ctypes.c_int), ("n", ctypes.c_int), ("g", ctypes.c_int), ("overlap", ctypes.c_int),
-                ("nstages", ctypes.c_int), ("stage", ctypes.c_int * MAX_STAGES),
-                ("op0", ctypes.c_int * MAX_STAGES), ("nops", ctypes.c_int * MAX_STAGES),
-                ("ops", ctypes.c_void_p)]
+class PackOp(ctypes.Structure):
+    _fields_ = [("boff", ctypes.c_longlong), ("field0", ctypes.c_int), ("nfield", ctypes.c_int),
+                ("y0", ctypes.c_int), ("ny", ctypes.c_int), ("z0", ctypes.c_int), ("nz", ctypes.c_int),
+                ("unpack", ctypes.c_int), ("reserved", ctypes.c_int)]
 
 
-XCHG_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(HaloOp), ctypes.c_int)
+class StagePlan(ctypes.Structure):
+    _fields_ = [(k, ctypes.c_int) for k in ("stage", "mode", "sweeps", "particle", "op0", "nops", "opb0", "nopsb",
+                                            "pk0", "npk", "run0", "nruns")]
+
+
+class SeriesEntry(ctypes.Structure):
+    _fields_ = [(k, ctypes.c_int) for k in ("idx", "dtidx", "len", "off")]
+
+
+class PartPlan(ctypes.Structure):
+    _fields_ = [("P", ctypes.c_void_p), ("acc", ctypes.c_void_p), ("m", ctypes.c_void_p), ("free_", ctypes.c_void_p),
+                ("n", ctypes.c_int), ("container", ctypes.c_int), ("grid", ctypes.c_void_p),
+                ("grid_n", ctypes.c_longlong), ("gdim", ctypes.c_int * 3), ("cell", ctypes.c_int),
+                ("ncell", ctypes.c_int), ("nl", ctypes.c_int), ("mscale", ctypes.c_double),
+                ("tmp", ctypes.c_void_p), ("tmp_bytes", ctypes.c_longlong), ("a", ctypes.c_double * 3),
+                ("period", ctypes.c_double * 3), ("periodic", ctypes.c_int), ("integrate", ctypes.c_int),
+                ("allreduce", ctypes.c_int), ("reserved", ctypes.c_int)]
+
+
+class LoopPlan(ctypes.Structure):
+    _fields_ = [("axis", ctypes.c_int), ("n", ctypes.c_int), ("g", ctypes.c_int),
+                ("ny", ctypes.c_int), ("nz", ctypes.c_int), ("gy", ctypes.c_int), ("gz", ctypes.c_int),
+                ("overlap", ctypes.c_int), ("nstages", ctypes.c_int), ("st", StagePlan * MAX_STAGES),
+                ("ops", ctypes.c_void_p), ("packs", ctypes.c_void_p), ("runs", ctypes.c_void_p),
+                ("scratch", ctypes.c_void_p), ("staging", ctypes.c_void_p), ("fs_bytes", ctypes.c_longlong),
+                ("nseries", ctypes.c_int), ("nsamplers", ctypes.c_int), ("series", ctypes.c_void_p),
+                ("svals", ctypes.c_void_p), ("sslopes", ctypes.c_void_p), ("zonal", ctypes.c_void_p),
+                ("samplers", ctypes.c_void_p), ("part", ctypes.c_void_p)]
+
+
+XCHG_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(HaloOp),
+                           ctypes.c_int)
+ALLRED_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_longlong)
 
 TRANSPORT_CODE = {"copy": 0, "rccl": 1, "callback": 2}
+_SIZES = (("plan", LoopPlan), ("stage", StagePlan), ("part", PartPlan), ("pack", PackOp), ("series", SeriesEntry))
 
 
 class NativeDistError(RuntimeError):
@@ -74,11 +114,13 @@ def _host_lib():
         from ..ops import host
         L = host.lib()
         P, i = ctypes.c_void_p, ctypes.c_int
-        L.tclb_dist_iterate_cpu.argtypes = [P, i, i, i, P, i, i, P, P, P, P, P]
-        L.tclb_dist_iterate_cpu.restype = i
-        if L.tclb_dist_sizeof_plan_cpu() != ctypes.sizeof(DistPlan) or \
-                L.tclb_dist_sizeof_op_cpu() != ctypes.sizeof(HaloOp):
-            raise NativeDistError("ABI mismatch of DistPlan/HaloOp in libtclb_host.so")
+        L.tclb_loop_iterate_cpu.argtypes = [P, i, i, i, i, i, P, i, i, P, P, P, P, P]
+        L.tclb_loop_iterate_cpu.restype = i
+        for name, st in _SIZES:
+            if getattr(L, f"tclb_loop_sizeof_{name}_cpu")() != ctypes.sizeof(st):
+                raise NativeDistError(f"ABI mismatch of the loop {name} struct in libtclb_host.so")
+        if L.tclb_dist_sizeof_op_cpu() != ctypes.sizeof(HaloOp):
+            raise NativeDistError("ABI mismatch of HaloOp in libtclb_host.so")
         _host = L
     return _host
 
@@ -95,12 +137,19 @@ def _dev_lib():
         L.tclb_dist_ctx_create.argtypes = [ctypes.c_char_p, i, i, i, P]
         L.tclb_dist_ctx_create.restype = P
         L.tclb_dist_ctx_destroy.argtypes = [P]
-        L.tclb_dist_iterate.argtypes = [P, P, i, i, i, P, P, P, P]
-        L.tclb_dist_iterate.restype = i
+        L.tclb_loop_iterate.argtypes = [P, P, i, i, i, i, i, P, P, P]
+        L.tclb_loop_iterate.restype = i
         L.tclb_dist_exchange.argtypes = [P, P, P, i, P]
         L.tclb_dist_exchange.restype = i
-        if L.tclb_dist_sizeof_plan() != ctypes.sizeof(DistPlan) or L.tclb_dist_sizeof_op() != ctypes.sizeof(HaloOp):
-            raise NativeDistError("ABI mismatch of DistPlan/HaloOp in libtclb_device.so")
+        L.tclb_dist_wait.argtypes = [P, P, i]
+        L.tclb_dist_wait.restype = i
+        L.tclb_part_tmp_bytes.argtypes = [i, i]
+        L.tclb_part_tmp_bytes.restype = ctypes.c_longlong
+        for name, st in _SIZES:
+            if getattr(L, f"tclb_loop_sizeof_{name}")() != ctypes.sizeof(st):
+                raise NativeDistError(f"ABI mismatch of the loop {name} struct in libtclb_device.so")
+        if L.tclb_dist_sizeof_op() != ctypes.sizeof(HaloOp):
+            raise NativeDistError("ABI mismatch of HaloOp in libtclb_device.so")
         _dev = L
     return _dev
 
@@ -150,113 +199,327 @@ def gpu_context(comm, transport: str, device: torch.device) -> int:
         return ctx
 
 
-class NativeDist:
-    """the native loop of one lattice (tclb_amd.lattice.Lattice) over its slab split"""
+def _runs(idx: List[int]) -> List[Tuple[int, int]]:
+    out: List[Tuple[int, int]] = []
+    for i in idx:
+        if out and out[-1][1] == i:
+            out[-1] = (out[-1][0], i + 1)
+        else:
+            out.append((i, i + 1))
+    return out
+
+
+def _carr(ctype, items):
+    a = (ctype * max(1, len(items)))()
+    for i, it in enumerate(items):
+        for k, v in it.items():
+            setattr(a[i], k, v)
+    return a
+
+
+_OPF = ("off", "bytes", "kind", "peer", "tag", "buf")
+
+
+class NativeLoop:
+    """the native action loop of one lattice (tclb_amd.lattice.Lattice): one rank or many,
+    slab or Y x Z grid"""
 
     def __init__(self, lat):
         self.lat = lat
         comm = lat.comm
         self.gpu = lat.is_gpu
-        self.transport = choose_transport(comm, self.gpu)
-        self.rank = comm.rank if isinstance(comm, TorchDistComm) else 0
-        self._plans: Dict[Tuple[int, ...], tuple] = {}
-        self.ctx = gpu_context(comm, self.transport, lat.device) if self.gpu else None
-        self._cb = XCHG_FN(self._exchange_cb) if (not self.gpu and self.transport == "callback") else None
+        self.multi = isinstance(comm, TorchDistComm)
+        self.transport = choose_transport(comm, self.gpu) if comm.distributed else "copy"
+        self.rank = comm.rank if self.multi else 0
+        self._plans: Dict[tuple, tuple] = {}
+        self.ctx = gpu_context(comm if comm.distributed else LoopbackComm(), self.transport, lat.device) \
+            if self.gpu else None
+        cb = not self.gpu and self.transport == "callback"
+        self._cb = XCHG_FN(self._exchange_cb) if cb else None
+        self._ared = ALLRED_FN(self._allreduce_cb) if cb else None
         self._cb_error: Optional[str] = None
+        self._staging: Optional[torch.Tensor] = None
+        self._part_tmp: Optional[torch.Tensor] = None
 
     @staticmethod
     def supported(lat) -> bool:
-        """slab split with every halo contiguous per field: z slabs, or y slabs of 2-D
-        lattices (one z plane)"""
+        """what the loop steps: one rank without ghosts, slab splits with every halo
+        contiguous per field (z slabs, or y slabs of 2-D lattices), and the Y x Z grid"""
         ax = lat.slab.axis
-        return lat.g > 0 and (ax == 2 or (ax == 1 and lat.NZ == 1))
+        if lat.g == 0:
+            return True
+        return ax == 3 or ax == 2 or (ax == 1 and lat.NZ == 1)
 
     # ------------------------------------------------------------------ plan
+    def _peers(self, axis: int) -> Tuple[int, int]:
+        return self.lat.slab.neighbours(axis) if self.multi else (0, 0)
+
     def ops_for(self, fields) -> list:
-        """the halo ops of one stage saving `fields` (see dist_loop.hpp for the order)"""
+        """the direct (contiguous plane) halo ops of one stage saving `fields`: along the
+        slab axis, or the z phase of the grid (see dist_loop.hpp for the order)"""
         lat = self.lat
-        ax = lat.slab.axis
-        g = lat.g
+        ax = 2 if lat.slab.axis == 3 else lat.slab.axis
+        g = lat.gz if lat.slab.axis == 3 else lat.g
         n = lat.shape[2] if ax == 2 else lat.shape[1]
         plane = lat.NY * lat.px if ax == 2 else lat.px
         es = lat.snaps[0].element_size()
-        if isinstance(lat.comm, TorchDistComm):
-            prev, nxt = lat.slab.neighbours(ax)
-        else:
-            prev = nxt = 0
+        prev, nxt = self._peers(ax)
         fs = set(fields)
-        lo = [i for i in lat.halo_lo if i in fs]        # read from below: my top planes go up
-        hi = [i for i in lat.halo_hi if i in fs]        # read from above: my bottom planes go down
+        lo_set, hi_set = lat.halo_sets[ax]
+        lo = [i for i in lo_set if i in fs]        # read from below: my top planes go up
+        hi = [i for i in hi_set if i in fs]        # read from above: my bottom planes go down
         b = g * plane * es
         ops = []
         for f in lo:
-            ops.append(((f * lat.fs + n * plane) * es, b, 0, nxt, f))
+            ops.append(((f * lat.fs + n * plane) * es, b, 0, nxt, f, 0))
         for f in hi:
-            ops.append(((f * lat.fs + g * plane) * es, b, 0, prev, TAG_HI + f))
+            ops.append(((f * lat.fs + g * plane) * es, b, 0, prev, TAG_HI + f, 0))
         for f in lo:
-            ops.append((f * lat.fs * es, b, 1, prev, f))
+            ops.append((f * lat.fs * es, b, 1, prev, f, 0))
         for f in hi:
-            ops.append(((f * lat.fs + (n + g) * plane) * es, b, 1, nxt, TAG_HI + f))
+            ops.append(((f * lat.fs + (n + g) * plane) * es, b, 1, nxt, TAG_HI + f, 0))
         return ops
 
-    def plan(self, stages: Tuple[int, ...]):
-        p = self._plans.get(stages)
-        if p is not None:
-            return p
+    def y_phase(self, fields, stg_off: int):
+        """the grid's y phase of one stage: rows [n, n+g) of the fields read from below go
+        up, rows [g, 2g) of those read from above go down, over the ghost-inclusive z
+        extent, through staging messages [send up][send down][recv below][recv above];
+        returns (ops, packs, bytes)"""
+        lat = self.lat
+        g, n = lat.gy, lat.shape[1]
+        es = lat.snaps[0].element_size()
+        prev, nxt = self._peers(1)
+        fs = set(fields)
+        lo_set, hi_set = lat.halo_sets[1]
+        lo = [i for i in lo_set if i in fs]
+        hi = [i for i in hi_set if i in fs]
+        per = lat.NZ * g * lat.px * es             # one field's rows
+        ops, packs = [], []
+        msgs, off = {}, stg_off
+        for name, flist in (("su", lo), ("sd", hi), ("rb", lo), ("ra", hi)):
+            msgs[name] = off
+            off += per * len(flist)
+
+        def pk(base, flist, y0, unpack):
+            o = base
+            for r0, r1 in _runs(flist):
+                packs.append({"boff": o, "field0": r0, "nfield": r1 - r0, "y0": y0, "ny": g, "z0": 0,
+                              "nz": lat.NZ, "unpack": unpack})
+                o += per * (r1 - r0)
+        if lo:
+            pk(msgs["su"], lo, n, 0)
+            ops.append((msgs["su"], per * len(lo), 0, nxt, TAG_Y, 1))
+        if hi:
+            pk(msgs["sd"], hi, g, 0)
+            ops.append((msgs["sd"], per * len(hi), 0, prev, TAG_Y + TAG_HI, 1))
+        if lo:
+            ops.append((msgs["rb"], per * len(lo), 1, prev, TAG_Y, 1))
+            pk(msgs["rb"], lo, 0, 1)
+        if hi:
+            ops.append((msgs["ra"], per * len(hi), 1, nxt, TAG_Y + TAG_HI, 1))
+            pk(msgs["ra"], hi, n + g, 1)
+        return ops, packs, off - stg_off
+
+    @staticmethod
+    def stage_mode(k: int, st) -> int:
+        """0 plain, 1 out of place (snapshot reads), 2 fixed point (lattice.py run_action)"""
+        if k > 0 and st.fixed_point:
+            return 2
+        if k > 0 and st.snapshot_reads:
+            return 1
+        return 0
+
+    def plan(self, action: str):
         lat = self.lat
         m = lat.model
+        key = (action, lat.g, lat.overlap)
+        p = self._plans.get(key)
+        if p is not None:
+            return p
+        stages = [m.stage_index(s) for s in m.action(action).stages]
         if len(stages) > MAX_STAGES:
             raise NativeDistError(f"action of {len(stages)} stages (max {MAX_STAGES})")
-        P = DistPlan()
-        P.axis = lat.slab.axis
-        P.n = lat.shape[2] if P.axis == 2 else lat.shape[1]
-        P.g = lat.g
+        P = LoopPlan()
+        ax = lat.slab.axis if lat.g > 0 else 0
+        P.axis = ax
         P.overlap = 1 if lat.overlap else 0
+        if ax in (1, 2):
+            P.n = lat.shape[2] if ax == 2 else lat.shape[1]
+            P.g = lat.g
+        elif ax == 3:
+            P.ny, P.nz, P.gy, P.gz = lat.shape[1], lat.shape[2], lat.gy, lat.gz
         P.nstages = len(stages)
-        allops = []
+        allops, allpacks, runs = [], [], []
+        stg_bytes = 0
+        need_scratch = False
         for k, si in enumerate(stages):
-            ops = self.ops_for(lat._saved_fields(m.stages[si]))
-            P.stage[k] = si
-            P.op0[k] = len(allops)
-            P.nops[k] = len(ops)
-            allops += ops
-        arr = (HaloOp * max(1, len(allops)))()
-        for i, (off, b, kind, peer, tag) in enumerate(allops):
-            arr[i].off, arr[i].bytes, arr[i].kind, arr[i].peer, arr[i].tag = off, b, kind, peer, tag
+            st = m.stages[si]
+            fields = lat._saved_fields(st)
+            mode = self.stage_mode(k, st)
+            need_scratch |= mode > 0
+            S = P.st[k]
+            S.stage, S.mode, S.sweeps = si, mode, FIXED_POINT_SWEEPS if mode == 2 else 1
+            S.particle = 1 if st.particle else 0
+            S.run0, S.nruns = len(runs), len(_runs(fields)) if mode > 0 else 0
+            if mode > 0:
+                runs += _runs(fields)
+            if ax > 0:
+                ops = self.ops_for(fields)
+                S.op0, S.nops = len(allops), len(ops)
+                allops += ops
+                if ax == 3:
+                    yops, ypk, yb = self.y_phase(fields, stg_bytes)
+                    S.opb0, S.nopsb = len(allops), len(yops)
+                    S.pk0, S.npk = len(allpacks), len(ypk)
+                    allops += yops
+                    allpacks += ypk
+                    stg_bytes += yb
+        arr = _carr(HaloOp, [dict(zip(_OPF, o)) for o in allops])
+        pks = _carr(PackOp, allpacks)
+        rarr = (ctypes.c_int * max(2, 2 * len(runs)))(*[v for r in runs for v in r])
         P.ops = ctypes.cast(arr, ctypes.c_void_p)
-        p = self._plans[stages] = (P, arr)
+        P.packs = ctypes.cast(pks, ctypes.c_void_p)
+        P.runs = ctypes.cast(rarr, ctypes.c_void_p)
+        P.fs_bytes = lat.fs * lat.snaps[0].element_size()
+        keep = [arr, pks, rarr]
+        if need_scratch:
+            sc = lat._scratch_snapshot()
+            P.scratch = sc.data_ptr()
+        if stg_bytes:
+            if self._staging is None or self._staging.numel() < stg_bytes:
+                self._staging = torch.zeros(stg_bytes, dtype=torch.uint8, device=lat.device)
+            P.staging = self._staging.data_ptr()
+        p = self._plans[key] = (P, keep)
         return p
 
+    # ------------------------------------------------------------------ per-call parts
+    def _series(self, P: LoopPlan, keep: list):
+        lat = self.lat
+        if not lat.zseries:
+            P.nseries = 0
+            return
+        nzs, nzones = lat.zvals.shape
+        ents, vals, slopes = [], [], []
+        for (zi, z), v in lat.zseries.items():
+            n = len(v)
+            for k in range(n):
+                lo, hi = max(k - 1, 0), min(k + 1, n - 1)
+                slopes.append((v[hi] - v[lo]) / max(hi - lo, 1))
+            ents.append({"idx": zi * nzones + z, "dtidx": nzs * nzones + zi * nzones + z, "len": n,
+                         "off": len(vals)})
+            vals += [float(x) for x in v]
+        E = _carr(SeriesEntry, ents)
+        if self.gpu:
+            Ed = torch.frombuffer(bytearray(bytes(E)), dtype=torch.uint8).to(lat.device)
+            keep.append(Ed)
+            P.series = Ed.data_ptr()
+        else:
+            keep.append(E)
+            P.series = ctypes.cast(E, ctypes.c_void_p)
+        vt = torch.tensor(vals, dtype=torch.float64, device=lat.device)
+        sl = torch.tensor(slopes, dtype=torch.float64, device=lat.device)
+        keep += [vt, sl]
+        P.nseries, P.svals, P.sslopes = len(ents), vt.data_ptr(), sl.data_ptr()
+        P.zonal = lat.zonal_t.data_ptr()
+
+    def _samplers(self, P: LoopPlan, n: int, keep: list):
+        smps = self.lat.samplers
+        P.nsamplers = len(smps)
+        if not smps:
+            P.samplers = None
+            return
+        arr = (abi.SamplePlan * len(smps))()
+        for i, s in enumerate(smps):
+            sp = s.plan_for(n)
+            ctypes.memmove(ctypes.byref(arr[i]), ctypes.byref(sp), ctypes.sizeof(abi.SamplePlan))
+        keep.append(arr)
+        P.samplers = ctypes.cast(arr, ctypes.c_void_p)
+
+    def _particles(self, P: LoopPlan, keep: list):
+        lat = self.lat
+        ps = lat.particles
+        if ps is None:
+            P.part = None
+            return
+        ps._ensure(lat)
+        d = ps._d
+        Q = PartPlan()
+        n = ps.n
+        Q.P, Q.acc, Q.m, Q.free_, Q.n = d["P"].data_ptr(), d["acc"].data_ptr(), d["m"].data_ptr(), \
+            d["free"].data_ptr(), n
+        kind = d["kind"]
+        Q.container = {None: 0, "grid": 1, "tree": 2}[kind]
+        if kind is not None:
+            Q.grid, Q.grid_n = d["grid"].data_ptr(), d["grid"].numel()
+        if kind == "grid":
+            Q.gdim[0], Q.gdim[1], Q.gdim[2] = d["gdim"]
+            Q.cell, Q.ncell = d["cell"], d["ncell"]
+        if kind == "tree":
+            Q.nl, Q.mscale = d["nl"], d["mscale"]
+        if kind is not None and self.gpu:
+            need = int(_dev_lib().tclb_part_tmp_bytes(n, Q.ncell if kind == "grid" else 0))
+            if self._part_tmp is None or self._part_tmp.numel() < need:
+                self._part_tmp = torch.empty(need, dtype=torch.uint8, device=lat.device)
+            Q.tmp, Q.tmp_bytes = self._part_tmp.data_ptr(), self._part_tmp.numel()
+        integ = ps.native_integrator()
+        if integ is not None:
+            Q.integrate = 1
+            for k in range(3):
+                Q.a[k], Q.period[k] = float(integ["a"][k]), float(integ["period"][k])
+            Q.periodic = int(integ["periodic"])
+        Q.allreduce = 1 if (lat.comm.distributed and lat.comm.size > 1) else 0
+        keep.append(Q)
+        P.part = ctypes.cast(ctypes.pointer(Q), ctypes.c_void_p)
+
     # ------------------------------------------------------------------ run
-    def iterate(self, L: abi.Launch, prec: int, n: int, stages, glob_last: bool, sp=None):
-        P, _ = self.plan(tuple(stages))
-        lib = self.lat.lib
+    def iterate(self, L: abi.Launch, n: int, action: str, glob_last: bool):
+        lat = self.lat
+        P, _ = self.plan(action)
+        keep: list = []
+        self._series(P, keep)
+        if action == "Init":
+            P.nsamplers, P.samplers = 0, None        # Init records no probe row (lattice.py init)
+        else:
+            self._samplers(P, n, keep)
+        self._particles(P, keep)
+        lib = lat.lib
         run = ctypes.cast(lib._run, ctypes.c_void_p)
         sample = ctypes.cast(lib._smp, ctypes.c_void_p)
-        spp = ctypes.byref(sp) if sp is not None else None
+        es = lat.snaps[0].element_size()
+        init = 1 if action == "Init" else 0
         if self.gpu:
-            r = _dev_lib().tclb_dist_iterate(self.ctx, ctypes.byref(L), prec, n, 1 if glob_last else 0,
-                                              ctypes.byref(P), run, sample, spp)
+            r = _dev_lib().tclb_loop_iterate(self.ctx, ctypes.byref(L), lat.prec, es, n, 1 if glob_last else 0, init,
+                                             ctypes.byref(P), run, sample)
             if r != 0:
-                raise NativeDistError(f"native multi-rank loop failed ({r}): {_err()}")
+                raise NativeDistError(f"native action loop failed ({r}): {_err()}")
             return
         self._cb_error = None
-        r = _host_lib().tclb_dist_iterate_cpu(ctypes.byref(L), prec, n, 1 if glob_last else 0, ctypes.byref(P),
-                                              TRANSPORT_CODE[self.transport], self.rank,
+        r = _host_lib().tclb_loop_iterate_cpu(ctypes.byref(L), lat.prec, es, n, 1 if glob_last else 0, init,
+                                              ctypes.byref(P), TRANSPORT_CODE[self.transport], self.rank,
                                               ctypes.cast(self._cb, ctypes.c_void_p) if self._cb else None,
-                                              None, run, sample, spp)
+                                              ctypes.cast(self._ared, ctypes.c_void_p) if self._ared else None,
+                                              None, run, sample)
         if r != 0:
-            raise NativeDistError(f"native multi-rank loop failed ({r})" +
+            raise NativeDistError(f"native action loop failed ({r})" +
                                   (f": {self._cb_error}" if self._cb_error else ""))
+
+    def wait(self, timeout_ms: Optional[int] = None):
+        """wait for this rank's queued work with the RCCL communicator watched (a dead peer
+        aborts the communicator and raises instead of hanging the rank)"""
+        if not self.gpu or self.transport != "rccl":
+            return
+        t = int(os.environ.get("TCLB_DIST_TIMEOUT_MS", "600000")) if timeout_ms is None else timeout_ms
+        stream = torch.cuda.current_stream(self.lat.device).cuda_stream
+        r = _dev_lib().tclb_dist_wait(self.ctx, stream, t)
+        if r != 0:
+            raise NativeDistError(f"native loop wait failed ({r}): {_err()}")
 
     def exchange(self, buf: torch.Tensor, fields):
         """one exchange of `fields` of snapshot `buf` through the native transport (GPU)"""
         ops = self.ops_for(fields)
         if not ops:
             return
-        arr = (HaloOp * len(ops))()
-        for i, (off, b, kind, peer, tag) in enumerate(ops):
-            arr[i].off, arr[i].bytes, arr[i].kind, arr[i].peer, arr[i].tag = off, b, kind, peer, tag
+        arr = _carr(HaloOp, [dict(zip(_OPF, o)) for o in ops])
         stream = torch.cuda.current_stream(self.lat.device).cuda_stream
         r = _dev_lib().tclb_dist_exchange(self.ctx, buf.data_ptr(), ctypes.cast(arr, ctypes.c_void_p), len(ops),
                                           stream)
@@ -270,18 +533,30 @@ class NativeDist:
                 return torch.as_strided(s, (lat.nf * lat.fs,), (1,), s.storage_offset())
         raise NativeDistError("exchange of an unknown snapshot")
 
-    def _exchange_cb(self, user, base, ops, nops) -> int:
-        """transport 'callback': one stage's ops as gloo isend/irecv"""
+    def _exchange_cb(self, user, base, staging, ops, nops) -> int:
+        """transport 'callback': one phase's ops as gloo isend/irecv"""
         try:
             comm = self.lat.comm
             d = comm.dist
             flat = self._flat(base)
             es = flat.element_size()
+            stg = self._staging
             p2p = []
+            # TCLB_DIST_ORDER_MATCH=1: pair sends and receives by issue order per peer (the
+            # k-th send to a peer with that peer's k-th receive from us), ignoring the plan's
+            # tags — the matching RCCL applies to a group of ncclSend/ncclRecv, rehearsed on
+            # gloo ranks (tests/test_distributed.py)
+            order = os.environ.get("TCLB_DIST_ORDER_MATCH", "0") == "1"
+            seq: Dict[Tuple[int, int], int] = {}
             for i in range(nops):
                 o = ops[i]
-                t = flat[o.off // es:(o.off + o.bytes) // es]
-                p2p.append(d.P2POp(d.isend if o.kind == 0 else d.irecv, t, comm._g(o.peer), comm.group, o.tag))
+                t = stg[o.off:o.off + o.bytes] if o.buf else flat[o.off // es:(o.off + o.bytes) // es]
+                tag = o.tag
+                if order:
+                    k = (o.kind, o.peer)
+                    tag = seq.get(k, 0)
+                    seq[k] = tag + 1
+                p2p.append(d.P2POp(d.isend if o.kind == 0 else d.irecv, t, comm._g(o.peer), comm.group, tag))
             for w in d.batch_isend_irecv(p2p):
                 w.wait()
             return 0
@@ -289,9 +564,24 @@ class NativeDist:
             self._cb_error = traceback.format_exc(limit=4)
             return -5
 
+    def _allreduce_cb(self, user, a, n) -> int:
+        """transport 'callback': sum of the particle force accumulator over the ranks"""
+        try:
+            acc = self.lat.particles._d["acc"]
+            if acc.data_ptr() != a or acc.numel() < n:
+                raise NativeDistError("all-reduce of an unknown buffer")
+            acc.copy_(self.lat.comm.allreduce_globals(acc.reshape(-1).clone(), acc.numel()).reshape(acc.shape))
+            return 0
+        except Exception:  # noqa: BLE001
+            self._cb_error = traceback.format_exc(limit=4)
+            return -6
+
+
+NativeDist = NativeLoop
+
 
 def native_dist_enabled() -> bool:
     return os.environ.get("TCLB_DIST_NATIVE", "1") != "0"
 
 
-__all__ = ["NativeDist", "NativeDistError", "native_dist_enabled", "choose_transport", "LoopbackComm"]
+__all__ = ["NativeLoop", "NativeDist", "NativeDistError", "native_dist_enabled", "choose_transport", "LoopbackComm"]

@@ -189,6 +189,9 @@ class RemoteParticles(ParticleSystem):
     free port, see ``.address``) and accepts one integrator; ``accept()`` completes the
     handshake."""
 
+    def native_ok(self) -> bool:
+        return False        # every particle stage exchanges with the integrator over the socket
+
     def __init__(self, address: str = "127.0.0.1:0", comm=None, units: Optional[dict] = None, box=None,
                  timeout: float = 120.0):
         super().__init__(0)

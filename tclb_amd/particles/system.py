@@ -196,6 +196,52 @@ class ParticleSystem:
             B[st:st + cnt, 3:6] = ch[:, :, 3:6].amax(1)
             lvl -= 1
 
+    def _build_native(self, lat):
+        """the solid container built by the native code the action loop also calls
+        (csrc/device/particles.hip on a GPU, csrc/runtime/particles_cpu.cpp on the CPU), so
+        the Python step path and the native loop share one implementation; _build_grid /
+        _build_tree above are the tensor-op statements of the same layouts (tests)"""
+        d, n = self._d, self.n
+        P, g = d["P"], d["grid"]
+        if P.is_cuda:
+            from ..ops import device as D
+            from ..parallel.native import _dev_lib
+            need = int(_dev_lib().tclb_part_tmp_bytes(n, d["ncell"] if d["kind"] == "grid" else 0))
+            if d.get("tmp") is None or d["tmp"].numel() < need:
+                d["tmp"] = torch.empty(need, dtype=torch.uint8, device=P.device)
+            t = d["tmp"]
+            if d["kind"] == "grid":
+                gx, gy, gz = d["gdim"]
+                r = D.lib().tclb_part_build_grid(P.data_ptr(), n, g.data_ptr(), gx, gy, gz, d["cell"], d["ncell"],
+                                                 t.data_ptr(), t.numel(), lat._stream())
+            else:
+                r = D.lib().tclb_part_build_tree(P.data_ptr(), n, g.data_ptr(), d["nl"], d["mscale"], t.data_ptr(),
+                                                 t.numel(), lat._stream())
+            if r != 0:
+                raise RuntimeError(f"solid container build failed ({r})")
+            return
+        from ..ops import host as H
+        if d["kind"] == "grid":
+            gx, gy, gz = d["gdim"]
+            H.lib().tclb_part_build_grid_cpu(P.data_ptr(), n, g.data_ptr(), gx, gy, gz, d["cell"], d["ncell"])
+        else:
+            H.lib().tclb_part_build_tree_cpu(P.data_ptr(), n, g.data_ptr(), d["nl"], d["mscale"])
+
+    # -- native action loop (parallel/native.py) ------------------------------------
+    def native_ok(self) -> bool:
+        """the native action loop can run this system's stage hooks itself (device-resident
+        records; no per-step host exchange with another program)"""
+        return True
+
+    def native_integrator(self):
+        """parameters of the rigid-body step the loop runs after each particle stage, or
+        None (particles that do not move)"""
+        return None
+
+    def after_native(self, lat, n: int, action: str):
+        """host bookkeeping after n native steps"""
+        self._host_stale |= {"force", "torque"}
+
     def _attach(self, lat, acc):
         d = self._d
         L = lat._L
@@ -203,7 +249,7 @@ class ParticleSystem:
         L.ext[3] = acc.data_ptr()
         L.next[2] = self.n
         if d["grid"] is not None:
-            self._build_tree() if d["kind"] == "tree" else self._build_grid()
+            self._build_native(lat)
             L.ext[4] = d["grid"].data_ptr()
             L.next[4] = d["grid"].numel()
         else:
@@ -234,7 +280,8 @@ class ParticleSystem:
             from ..ops import device as D
             D.nan_to_zero(acc, lat._stream())
         else:
-            acc.masked_fill_(torch.isnan(acc), 0.0)
+            from ..ops import host as H
+            H.lib().tclb_part_nan_to_zero_cpu(acc.data_ptr(), acc.numel())
         self._host_stale |= {"force", "torque"}
         self.detach(lat)
 
@@ -293,21 +340,28 @@ class SimplePart(ParticleSystem):
             D.rigid_step(d["P"], d["acc"], d["m"], d["free"], n, self.acc, bits, self.period, stream)
             self._host_stale |= {"x", "v", "omega"}
             return
-        P, acc = d["P"][:n], d["acc"][:n]
-        x, v, w, r = P[:, 0:3], P[:, 3:6], P[:, 6:9], P[:, 9]
-        m = d["m"][:n]
-        free = d["free"][:n, None]
-        a = torch.as_tensor(self.acc, dtype=torch.float64, device=P.device)
-        nv = v + (acc[:, 0:3] / m[:, None] + a)
-        nx = x + nv
-        nw = w + acc[:, 3:6] / (0.4 * m * r ** 2)[:, None]
-        for k in range(3):
-            if self.periodic[k] and self.period[k] > 0:
-                nx[:, k] = torch.remainder(nx[:, k], float(self.period[k]))
-        v.copy_(torch.where(free, nv, v))
-        x.copy_(torch.where(free, nx, x))
-        w.copy_(torch.where(free, nw, w))
+        # the host runtime's step (csrc/runtime/particles_cpu.cpp), the one the native
+        # action loop runs on the CPU
+        from ..ops import host as H
+        bits = sum(1 << k for k in range(3) if self.periodic[k])
+        H.lib().tclb_part_rigid_step_cpu(d["P"].data_ptr(), d["acc"].data_ptr(), d["m"].data_ptr(),
+                                         d["free"].data_ptr(), n, float(self.acc[0]), float(self.acc[1]),
+                                         float(self.acc[2]), bits, float(self.period[0]), float(self.period[1]),
+                                         float(self.period[2]))
         self._host_stale |= {"x", "v", "omega"}
+
+    def native_ok(self) -> bool:
+        return self.log_path is None          # the particle log is written from Python per step
+
+    def native_integrator(self):
+        return {"a": [float(v) for v in self.acc], "period": [float(v) for v in self.period],
+                "periodic": sum(1 << k for k in range(3) if self.periodic[k])}
+
+    def after_native(self, lat, n: int, action: str):
+        self._host_stale |= {"force", "torque"}
+        if action != "Init" and self.n:
+            self.iteration += n
+            self._host_stale |= {"x", "v", "omega"}
 
     def step(self, lat):
         self.iteration += 1

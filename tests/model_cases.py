@@ -70,10 +70,10 @@ def case_settings(name):
     return {}
 
 
-def make_case(name, device="cpu", precision="double", shape=None, comm=None):
+def make_case(name, device="cpu", precision="double", shape=None, comm=None, **kw):
     m = registry.get(name)
     shape = shape or (SMALL_2D if m.dims == 2 else SMALL_3D)
-    lat = Lattice(name, shape, device=torch.device(device), precision=precision, comm=comm)
+    lat = Lattice(name, shape, device=torch.device(device), precision=precision, comm=comm, **kw)
     nx = shape[0]
     fl = np.full((lat.NZ, lat.NY, nx), collision_value(m), dtype=np.uint32)
     wall = m.node_type("Wall")

@@ -172,3 +172,50 @@ def test_d3q19_adj_porosity_gradient():
     g[wi, :, :, 4:6] = 0.0
     lat.set_fields_interior(g)
     assert objective(lat, steps) < 0.5 * J0
+
+
+def test_late_reads_keep_segment_matches_checkpoint_only():
+    """A model whose later stages read a field before the action writes it (Model.late_reads:
+    d2q9_poison_boltzmann's subiter) depends on what the output snapshot held, the state two
+    steps back.  The reverse sweep's segment re-run (keep_segment) must reproduce that
+    (each fresh output buffer is seeded with it), so it equals the
+    checkpoint-only sweep, which re-runs every step through the A/B swap."""
+    from model_cases import CASE_SETTINGS
+    assert Lattice("d2q9_poison_boltzmann", (6, 10, 1)).model.late_reads("Iteration") == ["subiter"]
+
+    def case():
+        lat = Lattice("d2q9_poison_boltzmann", (6, 10, 1), device=torch.device("cpu"))
+        m = lat.model
+        fl = np.full((lat.NZ, lat.NY, 6), m.node_type("Collision").value, dtype=np.uint32)
+        fl[:, lat.gy + 0, :] = m.node_type("Wall").value
+        fl[:, lat.gy + 9, :] = m.node_type("Wall").value
+        lat.set_flags(fl)
+        for k, v in CASE_SETTINGS["d2q9_poison_boltzmann"].items():
+            lat.set_setting(k, v)
+        lat.init()
+        lat.iterate(3)
+        return lat
+
+    out, seen = [], []
+    for keep in (True, False):
+        lat = case()
+        ad = Adjoint(lat)
+        states = []
+        orig = ad.step_back
+
+        def spy(a, action="Iteration", state=None, other=None, **kw):
+            # the state each reverse step linearises about (the recomputed primal state)
+            s = state if state is not None else lat.snaps[lat.cur]
+            states.append(s[:, :, lat.gy:lat.gy + 10, :6].clone())
+            return orig(a, action, state=state, other=other, **kw)
+        ad.step_back = spy
+        gen = torch.Generator().manual_seed(5)
+        a_final = torch.randn(lat.snaps[0].shape, generator=gen, dtype=torch.float64)
+        a = ad.unsteady(8, checkpoint=4, a_final=a_final, keep_segment=keep)
+        out.append(a[:, :, lat.gy:lat.gy + 10, :6].clone())
+        seen.append(states)
+    assert torch.count_nonzero(out[0]) > 0
+    assert len(seen[0]) == len(seen[1]) == 8
+    for s0, s1 in zip(*seen):
+        assert torch.equal(s0, s1)                      # subiter included: it counts on from the real value
+    assert torch.allclose(out[0], out[1], rtol=1e-12, atol=1e-14), (out[0] - out[1]).abs().max()

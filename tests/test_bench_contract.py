@@ -77,3 +77,20 @@ def test_bench_window_holds_exactly_steps_iterations():
         assert out["iterations_timed"] == steps and out["steps"] == steps
         window = 32 * 16 * 16 * steps / (out["value"] * 1e6)          # seconds, from the MLUPS
         assert abs(out["ms_per_step"] * steps / 1e3 - window) <= 0.01 * window + 1e-7
+
+
+def test_bench_rank_failure_ends_the_job():
+    """one rank of `bench.py --gpus 2` dies (TCLB_BENCH_FAIL_RANK=1) while rank 0 waits in
+    a collective: the launcher tears the job down and exits non-zero in bounded time, with
+    no JSON line (a failed run reports nothing rather than a number)"""
+    import time
+    env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="1", TCLB_BENCH_FAIL_RANK="1")
+    env.pop("WORLD_SIZE", None)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--cpu", "--gpus", "2", "--shape", "32,16,16",
+           "--steps", "3", "--warmup", "1"]
+    t0 = time.time()
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
+    assert r.returncode != 0
+    assert time.time() - t0 < 240
+    assert not [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert "failing on purpose" in r.stderr
