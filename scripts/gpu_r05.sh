@@ -25,6 +25,11 @@ smoke) step "smoke" 300 $O/smoke.log python -c "import __graft_entry__ as g; g.s
 bench) step "bench fp64 20" 300 $O/bench20.json python bench.py --steps 20 --warmup 5 ;;
 split) step "tile split probe fp64" 600 $O/split_fp64.jsonl python tools/direction_probe.py --detail --repeat 3 --variants default ;;
 splitms) step "tile split probe mixed-shift" 600 $O/split_ms.jsonl python tools/direction_probe.py --detail --repeat 2 --variants default --precision mixed-shift ;;
+counterlist) step "rocprofv3 -L" 120 $O/counters_avail.txt rocprofv3 -L ;;
+place) step "placement probe torch" 300 $O/place_torch.jsonl python tools/placement_probe.py --k 6
+       step "placement probe torch (2)" 300 $O/place_torch2.jsonl python tools/placement_probe.py --k 6 ;;
+splitmodels) step "tile split heavy models" 900 $O/split_models.jsonl python tools/perf_models.py --models d3q27_cumulant,d3q19,d3q27_tePSM_per_NEBB,d3q27q27_cm_cht,d3q27_pf_velocity_thermo --n3 256 --steps 20 --rounds 2 --splits 0,2,3 --allow-invalid
+       step "tile split pf384" 900 $O/split_pf384.jsonl python tools/perf_models.py --models d3q27_pf_velocity --n3 384 --steps 20 --rounds 2 --splits 0,2,3 --allow-invalid --precision mixed-shift ;;
 *) echo "unknown step $WHAT"; exit 2 ;;
 esac
 done

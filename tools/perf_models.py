@@ -48,18 +48,23 @@ def main():
     ap.add_argument("--precision", default="double")
     ap.add_argument("--variants", default="", help="comma list of HIP build variants to A/B (interleaved)")
     ap.add_argument("--rounds", type=int, default=1)
+    ap.add_argument("--splits", default="", help="comma list of tile-window maps (Lattice.set_tile_split) to A/B")
     ap.add_argument("--glob-every-step", action="store_true", help="globals integrated on every step")
     ap.add_argument("--allow-invalid", action="store_true", help="exit 0 even when a run went non-finite")
     a = ap.parse_args()
     invalid = []
     variants = a.variants.split(",") if a.variants else [None]
+    splits = [int(k) for k in a.splits.split(",")] if a.splits else [None]
     names = a.models.split(",") if a.models else registry.names()
     dev = torch.device("cuda", 0)
-    for name, variant, rnd in [(n, v, r) for n in names for r in range(a.rounds) for v in variants]:
+    for name, variant, split, rnd in [(n, v, k, r) for n in names for r in range(a.rounds) for v in variants
+                                      for k in splits]:
         m = registry.get(name)
         shape = (a.n3, a.n3, a.n3) if m.dims == 3 else (a.n2, a.n2, 1)
         try:
             lat = Lattice(name, shape, device=dev, precision=a.precision, variant=variant)
+            if split is not None:
+                lat.set_tile_split(split)
             coll = collision_flag(m)
             lat.set_flags(np.full((lat.NZ, lat.NY, shape[0]), coll, dtype=np.uint32))
             # the model-family settings of the catalog tests (a physical case; some
@@ -84,7 +89,7 @@ def main():
             es = lat.snaps[0].element_size()
             nodes = shape[0] * shape[1] * shape[2]
             bpn = 2 * lat.nf * es + lat.flags.element_size()
-            print(json.dumps({"model": name, "variant": variant, "round": rnd, "glob_every_step": a.glob_every_step, "shape": shape, "fields": lat.nf, "stages": len(m.stages),
+            print(json.dumps({"model": name, "variant": variant, "split": lat.tile_split, "round": rnd, "glob_every_step": a.glob_every_step, "shape": shape, "fields": lat.nf, "stages": len(m.stages),
                               "ms": round(dt * 1e3, 3), "MLUPS": round(nodes / dt / 1e6, 1),
                               "GBps_meter": round(nodes * bpn / dt / 1e9, 1), "finite": ok}), flush=True)
             del lat
