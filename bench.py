@@ -229,6 +229,8 @@ def main():
             "globals_finite": chk["globals_finite"],
             "checks": chk,
             "iterations_timed": iters_timed,
+            "tile_split": lat.tile_split,
+            "placement": lat.placement,
             "host_ms_per_step": round(t_host / max(1, a.steps - 1) * 1e3, 4) if not a.glob_every_step else None,
             "host_enqueue_ms_per_step": round(t_enqueue * 1e3, 4),
             "loop": ("native-dist/" + lat._dist.transport) if (lat._dist is not None and lat.comm.distributed) else

@@ -30,6 +30,8 @@ place) step "placement probe torch" 300 $O/place_torch.jsonl python tools/placem
        step "placement probe torch (2)" 300 $O/place_torch2.jsonl python tools/placement_probe.py --k 6 ;;
 splitmodels) step "tile split heavy models" 900 $O/split_models.jsonl python tools/perf_models.py --models d3q27_cumulant,d3q19,d3q27_tePSM_per_NEBB,d3q27q27_cm_cht,d3q27_pf_velocity_thermo --n3 256 --steps 20 --rounds 2 --splits 0,2,3 --allow-invalid
        step "tile split pf384" 900 $O/split_pf384.jsonl python tools/perf_models.py --models d3q27_pf_velocity --n3 384 --steps 20 --rounds 2 --splits 0,2,3 --allow-invalid --precision mixed-shift ;;
+bench3) for i in 1 2 3; do step "bench fp64 20 #$i" 300 $O/bench20_$i.json python bench.py --steps 20 --warmup 5; done
+        step "bench mixed-shift 20" 300 $O/bench20_ms.json python bench.py --steps 20 --warmup 5 --precision mixed-shift ;;
 *) echo "unknown step $WHAT"; exit 2 ;;
 esac
 done

@@ -11,6 +11,11 @@
 //   mode 2  virtual memory API: hipMemCreate of the whole size at the recommended
 //           granularity, mapped into a range reserved at a 1 GiB-aligned address
 //
+// None of the modes gives a placement that is fast every time (the same mode ran 9.5 and
+// 11.8 ms per dispatch on different allocations), so the lattice ranks several candidates
+// by tclb_snap_probe — the streaming read / write speed of each — and keeps the fastest
+// pair (tclb_amd/lattice.py _alloc_snapshots).
+//
 // Each call returns 0 or a HIP error code; tclb_snap_free releases by the same mode.
 #include <hip/hip_runtime.h>
 
@@ -82,6 +87,55 @@ int vmm_free(void* p) {
 }
 
 }  // namespace
+
+namespace {
+
+// streaming probe of one snapshot candidate: K field planes `stride` elements apart read
+// (op 1, summed into a sink that is never written for finite data) or written with
+// non-temporal stores (op 2) — the memory pattern of the collide-stream kernels
+template <class T, int K>
+__global__ void __launch_bounds__(256) k_probe(T* buf, T* sink, long long n, long long stride, int op) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  if (op == 1) {
+    T s = 0;
+#pragma unroll
+    for (int k = 0; k < K; k++) s += buf[k * stride + i];
+    if (s == (T)-1.2345e30) sink[0] = s;
+  } else {
+#pragma unroll
+    for (int k = 0; k < K; k++) __builtin_nontemporal_store((T)0, buf + k * stride + i);
+  }
+}
+
+template <class T>
+int probe(void* buf, void* sink, long long n, long long stride, int K, int op, hipStream_t s) {
+  const dim3 b(256), g((unsigned)((n + 255) / 256));
+  T* p = (T*)buf;
+  T* q = (T*)sink;
+  // the nearest unrolled width not above K (the pattern, not every byte, is what is probed);
+  // fewer than 9 planes: one stream over all of them
+  if (K >= 27) k_probe<T, 27><<<g, b, 0, s>>>(p, q, n, stride, op);
+  else if (K >= 19) k_probe<T, 19><<<g, b, 0, s>>>(p, q, n, stride, op);
+  else if (K >= 9) k_probe<T, 9><<<g, b, 0, s>>>(p, q, n, stride, op);
+  else {
+    const long long m = (long long)(K - 1) * stride + n;
+    if ((m + 255) / 256 > 0x7fffffffLL) return (int)hipErrorInvalidValue;
+    k_probe<T, 1><<<dim3((unsigned)((m + 255) / 256)), b, 0, s>>>(p, q, m, 0, op);
+  }
+  return (int)hipGetLastError();
+}
+
+}  // namespace
+
+// op 1: read / op 2: write (zeros) of K planes of n elements (elem_bytes 8 or 4), stride apart
+extern "C" int tclb_snap_probe(void* buf, void* sink, long long n, long long stride, int K, int elem_bytes, int op,
+                               void* stream) {
+  if (n <= 0 || K <= 0 || (n + 255) / 256 > 0x7fffffffLL) return (int)hipErrorInvalidValue;
+  if (elem_bytes == 8) return probe<double>(buf, sink, n, stride, K, op, (hipStream_t)stream);
+  if (elem_bytes == 4) return probe<float>(buf, sink, n, stride, K, op, (hipStream_t)stream);
+  return (int)hipErrorInvalidValue;
+}
 
 extern "C" int tclb_snap_alloc(void** out, size_t bytes, int mode, int device) {
   if (!out || bytes == 0) return (int)hipErrorInvalidValue;

@@ -121,7 +121,8 @@ class Lattice:
         self.fs = plane + self.field_pad
         if self.fs >= 2 ** 31:
             raise ValueError("local field exceeds 2^31 elements; use more ranks")
-        self.snaps = [self.new_snapshot() for _ in range(2)]
+        self.placement = None
+        self.snaps = self._alloc_snapshots()
         self.cur = 0
         fdt = torch.int16 if m.flag_bits == 16 else torch.int32
         self.flags = torch.zeros((self.NZ, self.NY, self.px), dtype=fdt, device=self.device)
@@ -186,15 +187,54 @@ class Lattice:
             self._dist = NativeLoop(self)
 
     def _default_tile_split(self) -> int:
+        """4 windows (k = 2) for 3-D single-stage models of up to 32 fields (d3q27 fp64
+        512^3 +2-4 %, d3q27_cumulant / d3q19 256^3 +2-10 %); the linear order elsewhere
+        (multi-stage, LDS-tile and CHT models measured equal or slower, profiles/README.md
+        r05e)"""
         env = os.environ.get("TCLB_TILE_SPLIT")
         if env is not None and env != "":
             return max(0, min(15, int(env)))
+        m = self.model
+        act = m.action("Iteration")
+        if self.is_gpu and m.dims == 3 and act is not None and len(act.stages) == 1 and len(m.fields) <= 32:
+            return 2
         return 0
 
     def set_tile_split(self, k: int):
         """log2 of the tile windows of the GPU kernels (0: linear block order)"""
         self.tile_split = max(0, min(15, int(k)))
         self._L.tile_split = self.tile_split
+
+    def _alloc_snapshots(self) -> List[torch.Tensor]:
+        """the A/B pair.  On a GPU, for large snapshots, placement-aware: where a 29 GB
+        snapshot lands in HBM moves the streaming speed of the kernel that writes (or reads)
+        it by up to ~20 % (tools/direction_probe.py, tools/placement_probe.py: the same
+        d3q27 fp64 512^3 collide ran 9.5-11.8 ms per dispatch from one allocation to the
+        next), so K candidates (TCLB_PLACE_CANDIDATES, default 4, as many as fit) are
+        allocated at once, each timed by a streaming read and write of its field planes
+        (ops.device.snap_probe_ms), and the two fastest kept.  TCLB_PLACE=0: no probing;
+        TCLB_PLACE_MIN_GB: smallest snapshot probed (default 2)."""
+        if not self.is_gpu or os.environ.get("TCLB_PLACE", "1") == "0":
+            return [self.new_snapshot() for _ in range(2)]
+        es = torch.tensor([], dtype=self.sdtype).element_size()
+        nbytes = self.nf * self.fs * es
+        if nbytes < float(os.environ.get("TCLB_PLACE_MIN_GB", "2")) * 2 ** 30:
+            return [self.new_snapshot() for _ in range(2)]
+        free, _ = torch.cuda.mem_get_info(self.device)
+        k = min(int(os.environ.get("TCLB_PLACE_CANDIDATES", "4")), int(0.9 * free // nbytes))
+        if k < 3:
+            return [self.new_snapshot() for _ in range(2)]
+        from .ops.device import snap_probe_ms
+        cands = [self.new_snapshot() for _ in range(k)]
+        times = [snap_probe_ms(c, self.nf, self.fs) for c in cands]
+        order = sorted(range(k), key=lambda i: times[i][0] + times[i][1])
+        keep = sorted(order[:2])
+        self.placement = {"candidates": k, "read_write_ms": [[round(r, 4), round(w, 4)] for r, w in times],
+                          "kept": keep}
+        snaps = [cands[i] for i in keep]
+        del cands
+        torch.cuda.empty_cache()
+        return snaps
 
     def new_snapshot(self, uninit: bool = False) -> torch.Tensor:
         """a zeroed snapshot buffer with the layout of snaps[0/1] ([nf][NZ][NY][px], field

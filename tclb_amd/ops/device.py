@@ -38,6 +38,8 @@ def lib():
             L.tclb_part_build_grid.restype = i
             L.tclb_part_build_tree.argtypes = [P, i, P, i, d, P, ctypes.c_longlong, P]
             L.tclb_part_build_tree.restype = i
+            L.tclb_snap_probe.argtypes = [P, P, ctypes.c_longlong, ctypes.c_longlong, i, i, i, P]
+            L.tclb_snap_probe.restype = i
             L.tclb_snap_alloc.argtypes = [ctypes.POINTER(P), ctypes.c_size_t, i, i]
             L.tclb_snap_alloc.restype = i
             L.tclb_snap_free.argtypes = [P, i]
@@ -94,3 +96,27 @@ def snap_buffer(nbytes: int, mode: str, device):
     t = torch.as_tensor(blk, device=dev)
     assert t.data_ptr() == blk.ptr and t.numel() == nbytes
     return t
+
+
+def snap_probe_ms(buf, nf: int, fs: int, reps: int = 2):
+    """(read ms, write ms) of the nf field planes (fs elements apart) of snapshot candidate
+    `buf` (a device tensor): best of `reps` streaming passes (csrc/device/snapalloc.hip
+    tclb_snap_probe); the write pass leaves the planes zero"""
+    import torch
+    dev = buf.device
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    sink = torch.zeros(4, dtype=buf.dtype, device=dev)
+    es = buf.element_size()
+    out = []
+    for op in (1, 2):
+        best = float("inf")
+        for _ in range(reps):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            _check(lib().tclb_snap_probe(buf.data_ptr(), sink.data_ptr(), fs, fs, nf, es, op, stream),
+                   "snapshot probe")
+            e1.record()
+            e1.synchronize()
+            best = min(best, e0.elapsed_time(e1))
+        out.append(best)
+    return out[0], out[1]

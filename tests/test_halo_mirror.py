@@ -15,6 +15,7 @@ def _run(model, shape, mode, steps=6, monkeypatch=None):
         lat = Lattice(model, shape)
     else:
         monkeypatch.setenv("TCLB_HALO_MIRROR", "1" if mode == "mirror" else "0")
+        monkeypatch.setenv("TCLB_DIST_NATIVE", "0")       # the Python step path's border kernels
         lat = Lattice(model, shape, comm=LoopbackComm(exercise_dist_path=True), overlap=True)
     m = lat.model
     coll = next(t for t in m.node_types if t.group == "COLLISION")
