@@ -31,6 +31,7 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 from tclb_amd.lattice import Lattice  # noqa: E402
 from tclb_amd.ops.abi import PRECISIONS  # noqa: E402
 from tclb_amd.parallel.comm import init_distributed_from_env  # noqa: E402
+from tclb_amd.utils.guard import collision_check  # noqa: E402
 
 METRIC = "MLUPS (million lattice updates/sec) whole-node, d3q27 512^3, at 1/2/4/8 MI355X"
 
@@ -95,11 +96,14 @@ def physics_checks(lat: Lattice, comm, mass0: float, precision: str) -> dict:
     zinv = bool(torch.equal(s[:, lat.gz, lat.gy:lat.gy + ny, :nx], s[:, lat.gz + nz - 1, lat.gy:lat.gy + ny, :nx]))
     xinv = bool(torch.equal(s[:, lat.gz:lat.gz + nz, lat.gy:lat.gy + ny, 0],
                             s[:, lat.gz:lat.gz + nz, lat.gy:lat.gy + ny, nx - 1]))
+    # the MRT nodes collide (tclb_amd/utils/guard.py: a stream-only run passes the rest)
+    g = collision_check(lat)
+    coll = comm.allreduce_scalar(0.0 if g["collides"] else 1.0, "max") == 0.0
     zinv = comm.allreduce_scalar(0.0 if zinv else 1.0, "max") == 0.0
     xinv = comm.allreduce_scalar(0.0 if xinv else 1.0, "max") == 0.0
     ok_glob = comm.allreduce_scalar(0.0 if ok_glob else 1.0, "max") == 0.0
     return {"globals_finite": ok_glob, "mass_rel_drift": drift, "mass_ok": bool(np.isfinite(drift) and drift <= tol),
-            "z_invariant": zinv, "x_invariant": xinv}
+            "z_invariant": zinv, "x_invariant": xinv, "collides": coll, "collision_rel_diff": g["rel_diff"]}
 
 
 def main():
@@ -201,7 +205,7 @@ def main():
     nodes = shape[0] * shape[1] * shape[2]
     mlups = nodes * a.steps / dt / 1e6
     chk = physics_checks(lat, comm, mass0, a.precision)
-    ok = chk["globals_finite"] and chk["mass_ok"] and chk["z_invariant"] and chk["x_invariant"]
+    ok = chk["globals_finite"] and chk["mass_ok"] and chk["z_invariant"] and chk["x_invariant"] and chk["collides"]
     if rank == 0:
         es = lat.snaps[0].element_size()
         nf = lat.nf

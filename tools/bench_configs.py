@@ -23,6 +23,7 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from tclb_amd.lattice import Lattice  # noqa: E402
+from tclb_amd.utils.guard import collision_check  # noqa: E402
 
 
 def _time(lat, steps, warmup, glob_every=False):
@@ -100,6 +101,9 @@ def physics_checks(lat) -> dict:
     c = {"globals_finite": bool(all(np.isfinite(v) for v in lat.globals.values()))}
     s = lat.snaps[lat.cur]
     c["fields_finite"] = all(bool(torch.isfinite(s[i]).all().item()) for i in range(lat.nf))
+    # the flagged nodes collide (a run that only streams passes every other check)
+    g = collision_check(lat)
+    c["collides"], c["collision_rel_diff"], c["collision_nodes"] = g["collides"], g["rel_diff"], g["collision_nodes"]
     if lat.particles is not None:
         v = np.asarray(lat.particles.v, dtype=float)
         vmax = float(np.abs(v).max()) if v.size else 0.0

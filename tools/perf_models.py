@@ -15,6 +15,7 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 from model_cases import case_settings  # noqa: E402
 from tclb_amd.lattice import Lattice  # noqa: E402
 from tclb_amd.models import registry  # noqa: E402
+from tclb_amd.utils.guard import collision_check  # noqa: E402
 
 
 def state_finite(lat) -> bool:
@@ -49,6 +50,9 @@ def main():
     ap.add_argument("--variants", default="", help="comma list of HIP build variants to A/B (interleaved)")
     ap.add_argument("--rounds", type=int, default=1)
     ap.add_argument("--splits", default="", help="comma list of tile-window maps (Lattice.set_tile_split) to A/B")
+    ap.add_argument("--device", default="cuda")
+    ap.add_argument("--flag", default="", help="node type to flag every node with (default: the collision the "
+                                               "model's default build runs, collision_flag)")
     ap.add_argument("--glob-every-step", action="store_true", help="globals integrated on every step")
     ap.add_argument("--allow-invalid", action="store_true", help="exit 0 even when a run went non-finite")
     a = ap.parse_args()
@@ -56,7 +60,12 @@ def main():
     variants = a.variants.split(",") if a.variants else [None]
     splits = [int(k) for k in a.splits.split(",")] if a.splits else [None]
     names = a.models.split(",") if a.models else registry.names()
-    dev = torch.device("cuda", 0)
+    dev = torch.device("cuda", 0) if a.device == "cuda" else torch.device(a.device)
+
+    def sync():
+        if dev.type == "cuda":
+            torch.cuda.synchronize()
+
     for name, variant, split, rnd in [(n, v, k, r) for n in names for r in range(a.rounds) for v in variants
                                       for k in splits]:
         m = registry.get(name)
@@ -65,7 +74,7 @@ def main():
             lat = Lattice(name, shape, device=dev, precision=a.precision, variant=variant)
             if split is not None:
                 lat.set_tile_split(split)
-            coll = collision_flag(m)
+            coll = m.node_type(a.flag).value if a.flag else collision_flag(m)
             lat.set_flags(np.full((lat.NZ, lat.NY, shape[0]), coll, dtype=np.uint32))
             # the model-family settings of the catalog tests (a physical case; some
             # defaults, e.g. zero densities of the phase-field models, are not)
@@ -74,16 +83,18 @@ def main():
                     lat.set_setting(k, v)
             lat.init()
             lat.iterate(3, glob_last=False)
-            torch.cuda.synchronize()
+            sync()
             t = time.perf_counter()
             if a.glob_every_step:
                 for _ in range(a.steps):
                     lat.iterate(1, glob_last=True, reduce=False)
             else:
                 lat.iterate(a.steps, glob_last=True)
-            torch.cuda.synchronize()
+            sync()
             dt = (time.perf_counter() - t) / a.steps
             ok = state_finite(lat)
+            guard = collision_check(lat)
+            ok = ok and guard["collides"]
             if not ok:
                 invalid.append(name)
             es = lat.snaps[0].element_size()
@@ -91,7 +102,9 @@ def main():
             bpn = 2 * lat.nf * es + lat.flags.element_size()
             print(json.dumps({"model": name, "variant": variant, "split": lat.tile_split, "round": rnd, "glob_every_step": a.glob_every_step, "shape": shape, "fields": lat.nf, "stages": len(m.stages),
                               "ms": round(dt * 1e3, 3), "MLUPS": round(nodes / dt / 1e6, 1),
-                              "GBps_meter": round(nodes * bpn / dt / 1e9, 1), "finite": ok}), flush=True)
+                              "GBps_meter": round(nodes * bpn / dt / 1e9, 1), "valid": ok,
+                              "collides": guard["collides"], "collision_rel_diff": guard["rel_diff"],
+                              "collision_nodes": guard["collision_nodes"]}), flush=True)
             del lat
             torch.cuda.empty_cache()
         except Exception as e:  # noqa
