@@ -3,7 +3,13 @@ only).  The headline case — d3q27 MRT channel 512^3, fp64: 58 GB of snapshots,
 offsets past 2^31 bytes — is invariant in x and z (uniform init, walls only in y), so
 after 20 steps the first and last z planes and x columns must be bitwise equal, and the
 total mass must be conserved; the same for the fp32-storage (mixed-shift) layout and for
-the native multi-rank loop (RCCL send/receive to itself) on the 8-GPU slab shape."""
+the native multi-rank loop (RCCL send/receive to itself) on the 8-GPU slab shape.
+
+Invariance alone passes a collision that is wrong the same way everywhere (e.g. a field
+base that overflows and aliases two fields), so the values are pinned too: by x/z
+invariance the populations of any (x, z) column equal those of a thin lattice of the same
+height run by the independent CPU executor (g++ OpenMP build of the same node source), to
+rounding."""
 import os
 import sys
 
@@ -34,11 +40,36 @@ def _channel(shape, precision, comm=None):
     return lat, bench.physics_checks(lat, lat.comm, m0, precision)
 
 
+def _thin_column(precision, ny=512, steps=20):
+    """the channel's y profile from a thin CPU lattice (periodic x and z, 8 x ny x 2)"""
+    import bench
+    from tclb_amd.lattice import Lattice
+    lat = Lattice("d3q27", (8, ny, 2), device=torch.device("cpu"), precision=precision)
+    lat.set_flags(bench.channel_flags(lat))
+    lat.set_setting("nu", 0.02)
+    lat.set_setting("ForceX", 1e-6)
+    lat.init()
+    lat.iterate(steps)
+    return lat.fields_interior()[:, 0, :, 0].double()          # [field][y]
+
+
+def _check_column(lat, precision, x, z):
+    ref = _thin_column(precision)
+    col = lat.fields_interior()[:, z, :, x].double().cpu()     # f itself in every storage mode
+    scale = float(ref.abs().max())
+    tol = 1e-12 if precision == "double" else 1e-6
+    err = float((col - ref).abs().max()) / scale
+    assert err <= tol, (precision, err)
+    return err
+
+
 @gpu
 @needs
 @pytest.mark.parametrize("precision", ["double", "mixed-shift"])
 def test_headline_512_invariants(precision):
     lat, chk = _channel((512, 512, 512), precision)
+    _check_column(lat, precision, 300, 137)
+    assert chk["collides"], chk
     assert lat.fs * lat.snaps[0].element_size() * lat.nf > 2 ** 31
     assert chk["z_invariant"] and chk["x_invariant"], chk
     assert chk["mass_ok"] and chk["globals_finite"], chk
@@ -59,3 +90,4 @@ def test_native_dist_rccl_slab_invariants(monkeypatch):
     lat, chk = _channel((512, 512, 64), "double", comm=LoopbackComm(exercise_dist_path=True))
     assert lat._dist is not None and lat._dist.transport == "rccl"
     assert chk["z_invariant"] and chk["x_invariant"] and chk["mass_ok"], chk
+    _check_column(lat, "double", 17, 63)
