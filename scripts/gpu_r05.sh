@@ -32,6 +32,13 @@ splitmodels) step "tile split heavy models" 900 $O/split_models.jsonl python too
        step "tile split pf384" 900 $O/split_pf384.jsonl python tools/perf_models.py --models d3q27_pf_velocity --n3 384 --steps 20 --rounds 2 --splits 0,2,3 --allow-invalid --precision mixed-shift ;;
 bench3) for i in 1 2 3; do step "bench fp64 20 #$i" 300 $O/bench20_$i.json python bench.py --steps 20 --warmup 5; done
         step "bench mixed-shift 20" 300 $O/bench20_ms.json python bench.py --steps 20 --warmup 5 --precision mixed-shift ;;
+configs) step "bench_configs fp64" 900 $O/configs_fp64.jsonl python tools/bench_configs.py --steps 100 --warmup 5
+         step "bench_configs mixed-shift" 900 $O/configs_ms.jsonl python tools/bench_configs.py --steps 100 --warmup 5 --precision mixed-shift ;;
+partslab) step "part256 4-GPU slab shape, native loop, RCCL self-send" 300 $O/part_slab_rccl.jsonl python tools/bench_configs.py --configs part256 --shape 256,256,64 --loopback-dist --transport rccl --steps 200 --warmup 10
+          step "part256 4-GPU slab shape, Python step path" 300 $O/part_slab_py.jsonl env TCLB_DIST_NATIVE=0 python tools/bench_configs.py --configs part256 --shape 256,256,64 --loopback-dist --transport rccl --steps 200 --warmup 10
+          export TMPDIR=/tmp
+          step "part256 slab trace" 300 $O/part_slab_prof.log rocprofv3 --kernel-trace --stats -d $O/prof_part_slab -o run --output-format csv -- python3 tools/bench_configs.py --configs part256 --shape 256,256,64 --loopback-dist --transport rccl --steps 50 --warmup 5 ;;
+prodtests) step "production + native-loop GPU tests" 900 $O/pytest_prod.log python -u -m pytest tests/test_gpu_production.py tests/test_native_loop.py tests/test_bench_particle_case.py -v -m gpu --timeout 300 --timeout-method thread -p no:cacheprovider ;;
 *) echo "unknown step $WHAT"; exit 2 ;;
 esac
 done

@@ -14,7 +14,7 @@ sys.path.insert(0, os.path.join(ROOT, "tools"))
 
 def test_part256_case_stays_bounded():
     import bench_configs as bc
-    lat = bc.part256(64, "double", torch.device("cpu"))
+    lat = bc.part256((64, 64, 64), "double", torch.device("cpu"))
     ps = lat.particles
     assert abs(ps.m[0] / (4.0 / 3.0 * np.pi * ps.r[0] ** 3) - 2.0) < 1e-12
     vmax = 0.0
@@ -26,3 +26,5 @@ def test_part256_case_stays_bounded():
     assert vmax < bc.PARTICLE_VMAX, vmax
     chk = bc.physics_checks(lat)
     assert chk["globals_finite"] and chk["fields_finite"] and chk["particle_bounded"], chk
+    assert chk["collides"], chk
+    assert lat._native_path("Iteration") == "loop"          # particle stages in the native loop

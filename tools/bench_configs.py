@@ -39,18 +39,19 @@ def _time(lat, steps, warmup, glob_every=False):
     return time.perf_counter() - t
 
 
-def cavity(n, precision, dev):
-    lat = Lattice("auto_d3q19_BGK", (n, n, n), device=dev, precision=precision)
+def cavity(shape, precision, dev, comm=None):
+    nx, ny, nz = shape
+    lat = Lattice("auto_d3q19_BGK", shape, device=dev, precision=precision, comm=comm)
     m = lat.model
-    fl = np.full((lat.NZ, lat.NY, n), m.node_type("MRT").value, dtype=np.uint32)
+    fl = np.full((lat.NZ, lat.NY, nx), m.node_type("MRT").value, dtype=np.uint32)
     wall = m.node_type("Wall").value
     gz, gy = lat.gz, lat.gy
     fl[:, gy + 0, :] = wall
     fl[:, :, 0] = wall
-    fl[:, :, n - 1] = wall
+    fl[:, :, nx - 1] = wall
     fl[gz + 0, :, :] = wall
-    fl[gz + n - 1, :, :] = wall
-    fl[gz + 1:gz + n - 1, gy + n - 1, 1:n - 1] = m.node_type("NVelocity").value | m.node_type("MRT").value
+    fl[gz + nz - 1, :, :] = wall
+    fl[gz + 1:gz + nz - 1, gy + ny - 1, 1:nx - 1] = m.node_type("NVelocity").value | m.node_type("MRT").value
     lat.set_flags(fl)
     lat.set_setting("Viscosity", 0.01)
     lat.set_setting("Velocity", 0.05)
@@ -58,13 +59,14 @@ def cavity(n, precision, dev):
     return lat
 
 
-def pf384(n, precision, dev):
-    lat = Lattice("d3q27_pf_velocity", (n, n, n), device=dev, precision=precision)
-    fl = np.full((lat.NZ, lat.NY, n), lat.model.node_type("MRT").value, dtype=np.uint32)
+def pf384(shape, precision, dev, comm=None):
+    nx, ny, nz = shape
+    lat = Lattice("d3q27_pf_velocity", shape, device=dev, precision=precision, comm=comm)
+    fl = np.full((lat.NZ, lat.NY, nx), lat.model.node_type("MRT").value, dtype=np.uint32)
     lat.set_flags(fl)
     for k, v in {"Density_h": 1.0, "Density_l": 0.1, "sigma": 0.01, "Viscosity_l": 0.1, "Viscosity_h": 0.1,
-                 "M": 0.05, "BubbleType": 1.0, "IntWidth": 4.0, "Radius": n / 4,
-                 "CenterX": n / 2, "CenterY": n / 2, "CenterZ": n / 2}.items():
+                 "M": 0.05, "BubbleType": 1.0, "IntWidth": 4.0, "Radius": min(shape) / 4,
+                 "CenterX": nx / 2, "CenterY": ny / 2, "CenterZ": nz / 2}.items():
         lat.set_setting(k, v)
     lat.init()
     return lat
@@ -74,11 +76,13 @@ PARTICLE_DENSITY = 2.0
 PARTICLE_VMAX = 0.1     # lattice units / step: far above the initial 0.01, far below a blow-up
 
 
-def part256(n, precision, dev):
+def part256(shape, precision, dev, comm=None):
     from tclb_amd.particles import SimplePart
-    lat = Lattice("auto_d3q19_part", (n, n, n), device=dev, precision=precision)
+    nx, ny, nz = shape
+    n = nx
+    lat = Lattice("auto_d3q19_part", shape, device=dev, precision=precision, comm=comm)
     m = lat.model
-    fl = np.full((lat.NZ, lat.NY, n), m.node_type("MRT").value, dtype=np.uint32)
+    fl = np.full((lat.NZ, lat.NY, nx), m.node_type("MRT").value, dtype=np.uint32)
     lat.set_flags(fl)
     lat.set_setting("Viscosity", 0.05)
     lat.set_setting("ForceX", 1e-6)
@@ -87,9 +91,9 @@ def part256(n, precision, dev):
     # in.channel-particles:22-23); a lighter one (rho_p/rho_f < ~1) is beyond the stability
     # limit of the explicit coupling and blows up (round-3 verdict: 1e4 at r = 16 was 0.58)
     r = n / 16
-    ps.add(x=(n / 2, n / 2, n / 2), r=r, v=(0.01, 0, 0), m=PARTICLE_DENSITY * 4.0 / 3.0 * np.pi * r ** 3)
+    ps.add(x=(nx / 2, ny / 2, nz / 2), r=r, v=(0.01, 0, 0), m=PARTICLE_DENSITY * 4.0 / 3.0 * np.pi * r ** 3)
     ps.periodic[:] = True
-    ps.period[:] = n
+    ps.period[:] = shape
     lat.particles = ps
     lat.init()
     return lat
@@ -125,23 +129,44 @@ def main():
     ap.add_argument("--precision", default="double")
     ap.add_argument("--size", type=int, default=0, help="override lattice size")
     ap.add_argument("--glob-every-step", action="store_true", help="globals on every step")
+    ap.add_argument("--shape", default="", help="explicit lattice nx,ny,nz (overrides --size)")
+    ap.add_argument("--loopback-dist", action="store_true",
+                    help="one rank through the multi-rank path (a per-rank slab of an N-GPU run)")
+    ap.add_argument("--transport", default=None, choices=["rccl", "copy"])
     a = ap.parse_args()
+    if a.transport:
+        os.environ["TCLB_DIST_TRANSPORT"] = a.transport
     dev = torch.device("cuda", 0)
     invalid = []
     for name in a.configs.split(","):
         fn, n, desc = CONFIGS[name]
         n = a.size or n
-        lat = fn(n, a.precision, dev)
+        shape = tuple(int(v) for v in a.shape.split(",")) if a.shape else (n, n, n)
+        comm = None
+        if a.loopback_dist:
+            from tclb_amd.parallel.comm import LoopbackComm
+            comm = LoopbackComm(exercise_dist_path=True)
+        lat = fn(shape, a.precision, dev, comm=comm)
+        # host cost of a step on an idle queue (launches, events, RCCL group calls)
+        lat.iterate(2, glob_last=False)
+        torch.cuda.synchronize()
+        th = time.perf_counter()
+        lat.iterate(4, glob_last=False)
+        t_enq = (time.perf_counter() - th) / 4
+        torch.cuda.synchronize()
         dt = _time(lat, a.steps, a.warmup, a.glob_every_step)
-        nodes = n ** 3
+        nodes = shape[0] * shape[1] * shape[2]
         checks = physics_checks(lat)
-        out = {"config": name, "desc": desc, "model": lat.model.name, "lattice": [n, n, n],
+        out = {"config": name, "desc": desc, "model": lat.model.name, "lattice": list(shape),
                "precision": a.precision, "glob_every_step": a.glob_every_step, "steps": a.steps, "ms_per_step": round(dt / a.steps * 1e3, 4),
                "MLUPS": round(nodes * a.steps / dt / 1e6, 1),
                "fields": lat.nf, "stages": len(lat.model.action("Iteration").stages),
                "globals_finite": checks["globals_finite"], "checks": checks,
                "valid": all(v for k, v in checks.items() if isinstance(v, bool)),
-               "memory_GB": round(lat.memory_bytes() / 1e9, 2)}
+               "memory_GB": round(lat.memory_bytes() / 1e9, 2),
+               "host_enqueue_ms_per_step": round(t_enq * 1e3, 4),
+               "loop": {"lib": "native", "loop": "native-loop/" + (lat._dist.transport if lat._dist else "?"),
+                        None: "python"}[lat._native_path("Iteration")]}
         print(json.dumps(out), flush=True)
         if not out["valid"]:
             invalid.append(name)
