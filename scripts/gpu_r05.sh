@@ -39,6 +39,13 @@ partslab) step "part256 4-GPU slab shape, native loop, RCCL self-send" 300 $O/pa
           export TMPDIR=/tmp
           step "part256 slab trace" 300 $O/part_slab_prof.log rocprofv3 --kernel-trace --stats -d $O/prof_part_slab -o run --output-format csv -- python3 tools/bench_configs.py --configs part256 --shape 256,256,64 --loopback-dist --transport rccl --steps 50 --warmup 5 ;;
 prodtests) step "production + native-loop GPU tests" 900 $O/pytest_prod.log python -u -m pytest tests/test_gpu_production.py tests/test_native_loop.py tests/test_bench_particle_case.py -v -m gpu --timeout 300 --timeout-method thread -p no:cacheprovider ;;
+adjoint) step "adjoint GPU tests" 600 $O/pytest_adjoint.log python -u -m pytest tests/test_adjoint_native.py tests/test_adjoint_reverse.py tests/test_adjoint.py -v -m gpu --timeout 300 --timeout-method thread -p no:cacheprovider
+         for m in d3q19_adj d3q19_heat_adj; do
+           step "bench adjoint $m native" 300 $O/adj_${m}_native.json python tools/bench_adjoint.py --model $m --size 128 --steps 80
+           step "bench adjoint $m python" 300 $O/adj_${m}_python.json env TCLB_AD_NATIVE=0 python tools/bench_adjoint.py --model $m --size 128 --steps 80
+         done
+         step "bench adjoint d2q9_adj native" 300 $O/adj_d2q9_adj_native.json python tools/bench_adjoint.py --model d2q9_adj --size 2048 --steps 80
+         step "bench adjoint d2q9_adj python" 300 $O/adj_d2q9_adj_python.json env TCLB_AD_NATIVE=0 python tools/bench_adjoint.py --model d2q9_adj --size 2048 --steps 80 ;;
 *) echo "unknown step $WHAT"; exit 2 ;;
 esac
 done

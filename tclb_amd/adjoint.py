@@ -21,6 +21,7 @@ from __future__ import annotations
 
 import ctypes
 import math
+import os
 from typing import Dict, List, Optional, Sequence
 
 import numpy as np
@@ -32,6 +33,13 @@ from .ops import abi
 
 class AdjointError(RuntimeError):
     pass
+
+
+class _AdSegPlan(ctypes.Structure):
+    """mirror of tclb::AdSegPlan (csrc/include/tclb_rt/ad_loop.hpp)"""
+    _fields_ = [("nsteps", ctypes.c_int), ("par0", ctypes.c_int), ("dual_count", ctypes.c_int),
+                ("mode", ctypes.c_int), ("states", ctypes.c_void_p), ("iters", ctypes.c_void_p),
+                ("abuf", ctypes.c_void_p * 2), ("ctx", ctypes.c_void_p * 2), ("abytes", ctypes.c_longlong)]
 
 
 class Adjoint:
@@ -67,6 +75,7 @@ class Adjoint:
         self._ctx_devs = ([self._ctx_dev, torch.zeros_like(self._ctx_dev)] if self._ctx_dev is not None
                           else [None, None])
         self._ovf = torch.zeros(1, dtype=torch.int32, device=dev) if lat.is_gpu else None
+        self.native_steps = 0         # reverse steps run by the native segment loop
 
     # ------------------------------------------------------------------ one action
     def _ad_stage(self, si: int, inp: torch.Tensor, aout: torch.Tensor, obj_weight: float) -> torch.Tensor:
@@ -90,18 +99,7 @@ class Adjoint:
                 self._abuf[0].copy_(aout)
         aout_b, ain = self._abuf[par], self._abuf[1 - par]
         ain.zero_()
-        L = lat._base_launch()
-        lat._sync_settings()
-        L.settings = lat.settings_t.data_ptr()
-        L.zonal = lat.zonal_t.data_ptr()
-        L.nzones = lat.zvals.shape[1]
-        L.flags = lat.flags.data_ptr()
-        L.in_ = inp.data_ptr()
-        L.out = self.scratch.data_ptr()
-        L.stage = si
-        L.glob = 1
-        L.iter = lat.iter
-        L.globals_ = lat.globals_t.data_ptr()
+        L = self._stage_launch(si, inp)
         c = self.ctx
         c.aout = aout_b.data_ptr()
         c.ain = ain.data_ptr()
@@ -112,7 +110,6 @@ class Adjoint:
         c.obj_weight = obj_weight
         c.overflow = 0
         c.reserved = 0
-        L.reserved2 = 0
         # GPU: tangent windows up to the largest input count a node of this stage read in an
         # earlier call (0 = all TCLB_AD_K); the device reports the count in AdCtx.reserved
         cover = self._ad_cover.get(si, 0) if self._ctx_dev is not None else 0
@@ -124,7 +121,6 @@ class Adjoint:
         # wave mixes the two (executor_ad_hip.hpp)
         rev = self.reverse and not self._seeded
         L.next[5] = 1 if rev else 0
-        L.stream = lat._stream()
         first = si not in self._ad_cover
         if self._ctx_dev is not None:
             raw = bytes(c)
@@ -136,13 +132,6 @@ class Adjoint:
             L.ext[5] = dev_ctx.data_ptr()
         else:
             L.ext[5] = ctypes.cast(ctypes.pointer(c), ctypes.c_void_p)
-        if lat.turb_t is not None:
-            L.ext[0] = lat.turb_t.data_ptr()
-            L.next[0] = lat.turb_t.shape[0]
-            L.time_shift = lat.turb_time_wn
-        if lat.cuts is not None:
-            L.ext[1] = lat.cuts.data_ptr()
-            L.next[1] = lat.cuts.numel()
         if rev and self._ctx_dev is not None:
             if self._dual_flags != lat.flags_version:
                 self._dual_bufs.clear()
@@ -193,6 +182,125 @@ class Adjoint:
             raise AdjointError(f"model {lat.model.name}: a node needed more than {self.lib.tangents} AD tangents")
         lat.reverse_halo(ain)
         return ain
+
+    def _stage_launch(self, si: int, inp: torch.Tensor) -> abi.Launch:
+        """the Launch of one AD stage call (everything but the executor context / mode)"""
+        lat = self.lat
+        L = lat._base_launch()
+        lat._sync_settings()
+        L.settings = lat.settings_t.data_ptr()
+        L.zonal = lat.zonal_t.data_ptr()
+        L.nzones = lat.zvals.shape[1]
+        L.flags = lat.flags.data_ptr()
+        L.in_ = inp.data_ptr()
+        L.out = self.scratch.data_ptr()
+        L.stage = si
+        L.glob = 1
+        L.iter = lat.iter
+        L.globals_ = lat.globals_t.data_ptr()
+        L.reserved2 = 0
+        L.stream = lat._stream()
+        if lat.turb_t is not None:
+            L.ext[0] = lat.turb_t.data_ptr()
+            L.next[0] = lat.turb_t.shape[0]
+            L.time_shift = lat.turb_time_wn
+        if lat.cuts is not None:
+            L.ext[1] = lat.cuts.data_ptr()
+            L.next[1] = lat.cuts.numel()
+        return L
+
+    def _native_ready(self, action: str) -> bool:
+        """the executor of the action's (single) stage has been sized by a first call"""
+        m = self.lat.model
+        act = m.action(action)
+        if len(act.stages) != 1:
+            return False
+        si = m.stage_index(act.stages[0])
+        if self._ctx_dev is None:
+            return True                  # the CPU executor needs no sizing
+        if si not in self._ad_cover:
+            return False
+        return not (self.reverse and not self._seeded and si not in self._dual_count)
+
+    def _segment_native(self, a: torch.Tensor, states: List[torch.Tensor], iters: List[int],
+                        action: str, obj_weight: float = 1.0) -> Optional[torch.Tensor]:
+        """the reverse steps of one checkpoint segment in one native call
+        (tclb_rt/ad_loop.hpp ad_segment): states[i] / iters[i] are the input state and
+        iteration of the i-th reverse step.  Taken for single-stage actions that save every
+        field, on a rank without ghost planes and without zonal series, once the stage's
+        executor sizing is known (its first call, through _ad_stage); None otherwise."""
+        lat = self.lat
+        m = lat.model
+        act = m.action(action)
+        if (len(act.stages) != 1 or lat.g != 0 or lat.zseries or not states or self._abuf is None
+                or os.environ.get("TCLB_AD_NATIVE", "1") == "0"):
+            return None
+        si = m.stage_index(act.stages[0])
+        gpu = self._ctx_dev is not None
+        if len(lat._saved_fields(m.stage(act.stages[0]))) != lat.nf or not self._native_ready(action):
+            return None
+        rev = self.reverse and not self._seeded
+        if a is self._abuf[1]:
+            par0 = 1
+        else:
+            par0 = 0
+            if a is not self._abuf[0]:
+                self._abuf[0].copy_(a)
+        L = self._stage_launch(si, states[0])
+        cover = self._ad_cover.get(si, 0) if gpu else 0
+        L.reserved0 = max(0, cover)
+        # one executor context per parity: aout = abuf[par], ain = abuf[1 - par]
+        ctxs = []
+        for par in (0, 1):
+            c = abi.AdCtx.from_buffer_copy(bytes(self.ctx))
+            c.aout, c.ain = self._abuf[par].data_ptr(), self._abuf[1 - par].data_ptr()
+            c.gset, c.gzon = self.gset.data_ptr(), self.gzon.data_ptr()
+            c.set_mask, c.zon_mask = self.set_mask.data_ptr(), self.zon_mask.data_ptr()
+            c.obj_weight, c.overflow, c.reserved = obj_weight, 0, 0
+            if gpu:
+                raw = bytes(c)
+                if raw != self._ctx_bytes[par]:
+                    self._ctx_devs[par].copy_(torch.frombuffer(bytearray(raw), dtype=torch.uint8))
+                    self._ctx_bytes[par] = raw
+                ctxs.append(self._ctx_devs[par].data_ptr())
+            else:
+                ctxs.append(c)
+        P = _AdSegPlan()
+        n = len(states)
+        P.nsteps, P.par0 = n, par0
+        if rev:
+            P.mode = 1
+            P.dual_count = self._dual_count.get(si, 0) if gpu else 0
+            if gpu:
+                L.aux = self._dual_bufs[si].data_ptr()
+            else:
+                P.mode = 2               # CPU: one pass, reverse or dual per node (next[5] = 1)
+        st = (ctypes.c_longlong * n)(*[s.data_ptr() for s in states])
+        it = (ctypes.c_int * n)(*iters)
+        P.states = ctypes.cast(st, ctypes.c_void_p)
+        P.iters = ctypes.cast(it, ctypes.c_void_p)
+        P.abuf[0], P.abuf[1] = self._abuf[0].data_ptr(), self._abuf[1].data_ptr()
+        for par in (0, 1):
+            P.ctx[par] = ctxs[par] if gpu else ctypes.cast(ctypes.pointer(ctxs[par]), ctypes.c_void_p).value
+        P.abytes = self._abuf[0].numel() * self._abuf[0].element_size()
+        run = ctypes.cast(self.lib._adj, ctypes.c_void_p)
+        if gpu:
+            from .parallel.native import _dev_lib
+            r = _dev_lib().tclb_ad_segment(ctypes.byref(L), ctypes.byref(P), run)
+        else:
+            from .parallel.native import _host_lib
+            r = _host_lib().tclb_ad_segment_cpu(ctypes.byref(L), ctypes.byref(P), run)
+        if r != 0:
+            raise AdjointError(f"native adjoint segment failed ({r})")
+        self.native_steps += n
+        if gpu:
+            o = abi.ADCTX_OVERFLOW_OFFSET
+            for par in (0, 1):
+                flag = self._ctx_devs[par][o:o + 4].view(torch.int32)
+                torch.maximum(self._ovf, flag, out=self._ovf)
+        elif any(c.overflow for c in ctxs):
+            raise AdjointError(f"model {lat.model.name}: a node needed more than {self.lib.tangents} AD tangents")
+        return self._abuf[1 - (par0 ^ ((n - 1) & 1))]
 
     def _free_bytes(self) -> float:
         if self.lat.is_gpu:
@@ -338,7 +446,23 @@ class Adjoint:
                     lat.snaps[1 - lat.cur] = lat.new_snapshot(uninit)
                 lat.iterate(1, glob_last=False, action=action)
                 states.append(lat.snaps[lat.cur])
-            for t in range(end - 1, base - 1, -1):
+            t_lo = end - 1
+            if keep_segment and not lat.zseries and len(lat.model.action(action).stages) == 1:
+                # the reverse steps of the segment in one native call; a stage the executor
+                # has not run yet goes through _ad_stage once first (it sizes the windows)
+                seg = list(range(end - 1, base - 1, -1))
+                if not self._native_ready(action):
+                    t = seg.pop(0)
+                    lat.iter = it0 + t
+                    a = self.step_back(a, action, state=states[t - base], _buffer=True)
+                r = self._segment_native(a, [states[t - base] for t in seg], [it0 + t for t in seg], action) \
+                    if seg else None
+                if r is not None or not seg:
+                    a = r if r is not None else a
+                    t_lo = base - 1
+                else:
+                    t_lo = seg[0]
+            for t in range(t_lo, base - 1, -1):
                 other = None
                 if keep_segment:
                     state = states[t - base]

@@ -20,6 +20,7 @@
 
 #include <chrono>
 
+#include "tclb_rt/ad_loop.hpp"
 #include "tclb_rt/dist_loop.hpp"
 
 namespace {
@@ -420,6 +421,15 @@ int tclb_dist_wait(void* ctx, void* stream, int timeout_ms) {
   (void)hipEventDestroy(e);
   return r;
 }
+
+// the reverse sweep of one checkpoint segment (tclb_rt/ad_loop.hpp) on the GPU
+int tclb_ad_segment(const tclb::Launch* L, const tclb::AdSegPlan* P, tclb::ad_run_fn run) {
+  hipStream_t s = (hipStream_t)L->stream;
+  return tclb::ad_segment(*L, *P, run, [&](void* p, long long b) {
+    return hip_check(hipMemsetAsync(p, 0, (size_t)b, s), "hipMemsetAsync");
+  });
+}
+int tclb_ad_sizeof_seg() { return (int)sizeof(tclb::AdSegPlan); }
 
 int tclb_loop_sizeof_plan() { return (int)sizeof(tclb::LoopPlan); }
 int tclb_loop_sizeof_stage() { return (int)sizeof(tclb::StagePlan); }

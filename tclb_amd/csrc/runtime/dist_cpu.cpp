@@ -10,6 +10,7 @@
 #include <math.h>
 #include <string.h>
 
+#include "tclb_rt/ad_loop.hpp"
 #include "tclb_rt/dist_loop.hpp"
 
 extern "C" int tclb_part_build_grid_cpu(const double*, int, int*, int, int, int, int, int);
@@ -139,6 +140,15 @@ int tclb_loop_iterate_cpu(const tclb::Launch* L, int prec, int es, int nsteps, i
   CpuSvc sv{prec, run, sample, transport, rank, cb, ared, user, es, L->fs, L->sz, L->sy, L->px};
   return tclb::action_loop(sv, *L, nsteps, glob_last, *P, init);
 }
+
+// the reverse sweep of one checkpoint segment (tclb_rt/ad_loop.hpp), OpenMP AD executor
+int tclb_ad_segment_cpu(const tclb::Launch* L, const tclb::AdSegPlan* P, tclb::ad_run_fn run) {
+  return tclb::ad_segment(*L, *P, run, [](void* p, long long b) {
+    memset(p, 0, (size_t)b);
+    return 0;
+  });
+}
+int tclb_ad_sizeof_seg_cpu() { return (int)sizeof(tclb::AdSegPlan); }
 
 int tclb_loop_sizeof_plan_cpu() { return (int)sizeof(tclb::LoopPlan); }
 int tclb_loop_sizeof_stage_cpu() { return (int)sizeof(tclb::StagePlan); }

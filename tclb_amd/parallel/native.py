@@ -116,6 +116,8 @@ def _host_lib():
         P, i = ctypes.c_void_p, ctypes.c_int
         L.tclb_loop_iterate_cpu.argtypes = [P, i, i, i, i, i, P, i, i, P, P, P, P, P]
         L.tclb_loop_iterate_cpu.restype = i
+        L.tclb_ad_segment_cpu.argtypes = [P, P, P]
+        L.tclb_ad_segment_cpu.restype = i
         for name, st in _SIZES:
             if getattr(L, f"tclb_loop_sizeof_{name}_cpu")() != ctypes.sizeof(st):
                 raise NativeDistError(f"ABI mismatch of the loop {name} struct in libtclb_host.so")
@@ -139,6 +141,8 @@ def _dev_lib():
         L.tclb_dist_ctx_destroy.argtypes = [P]
         L.tclb_loop_iterate.argtypes = [P, P, i, i, i, i, i, P, P, P]
         L.tclb_loop_iterate.restype = i
+        L.tclb_ad_segment.argtypes = [P, P, P]
+        L.tclb_ad_segment.restype = i
         L.tclb_dist_exchange.argtypes = [P, P, P, i, P]
         L.tclb_dist_exchange.restype = i
         L.tclb_dist_wait.argtypes = [P, P, i]

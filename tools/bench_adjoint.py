@@ -155,7 +155,8 @@ def main():
                       "adjoint_cold_over_primal": round(tc / tp, 2),
                       "adjoint_MLUPS": round(nodes * a.steps / ta / 1e6, 2),
                       "J": ad.J, "grad_w_absmax": float(np.abs(g).max()), "finite": ok,
-                      "tangent_budget": ad.lib.tangents}), flush=True)
+                      "tangent_budget": ad.lib.tangents, "native_segment_steps": ad.native_steps,
+                      "native": os.environ.get("TCLB_AD_NATIVE", "1") != "0"}), flush=True)
     if not ok:
         sys.exit(3)
 
