@@ -46,6 +46,10 @@ adjoint) step "adjoint GPU tests" 600 $O/pytest_adjoint.log python -u -m pytest 
          done
          step "bench adjoint d2q9_adj native" 300 $O/adj_d2q9_adj_native.json python tools/bench_adjoint.py --model d2q9_adj --size 2048 --steps 80
          step "bench adjoint d2q9_adj python" 300 $O/adj_d2q9_adj_python.json env TCLB_AD_NATIVE=0 python tools/bench_adjoint.py --model d2q9_adj --size 2048 --steps 80 ;;
+addiag) for v in default row_w2 row_w2_wpe2 row row_wpe2 flat_wpe2; do
+          vv=$v; [ $v = default ] && vv=""
+          step "adjoint diag $v" 300 $O/addiag_$v.jsonl env TCLB_AD_VARIANT=$vv python tools/adjoint_diag.py --repeats 2
+        done ;;
 *) echo "unknown step $WHAT"; exit 2 ;;
 esac
 done

@@ -76,7 +76,18 @@ AD_VARIANTS = {f"w{w}": [f"-DTCLB_AD_WINDOW={w}"] for w in (1, 2, 3, 5)}
 AD_VARIANTS.update({"row": ["-DTCLB_FLAT_NODE=0"], "row_o1": ["-DTCLB_FLAT_NODE=0", "-O1"],
                     "row_w1": ["-DTCLB_FLAT_NODE=0", "-DTCLB_AD_WINDOW=1"],
                     "row_w2": ["-DTCLB_FLAT_NODE=0", "-DTCLB_AD_WINDOW=2"],
-                    "row_w3": ["-DTCLB_FLAT_NODE=0", "-DTCLB_AD_WINDOW=3"]})
+                    "row_w3": ["-DTCLB_FLAT_NODE=0", "-DTCLB_AD_WINDOW=3"],
+                    # round-5 diagnosis: the same row-form builds with VGPR->AGPR spilling off
+                    # (the failing builds are the ones whose k_ad runs past 256 VGPRs into AGPRs)
+                    # (the flag leaves the code unchanged: the AGPRs are allocated as ordinary
+                    # registers, not spill slots, profiles/README.md r05i) and with a 2-wave
+                    # floor that keeps k_ad within 256 VGPRs (no AGPRs at all)
+                    "row_noagpr": ["-DTCLB_FLAT_NODE=0", "-mllvm", "-amdgpu-spill-vgpr-to-agpr=0"],
+                    "row_w2_noagpr": ["-DTCLB_FLAT_NODE=0", "-DTCLB_AD_WINDOW=2", "-mllvm",
+                                      "-amdgpu-spill-vgpr-to-agpr=0"],
+                    "row_w2_wpe2": ["-DTCLB_FLAT_NODE=0", "-DTCLB_AD_WINDOW=2", "-DTCLB_AD_WAVES=2"],
+                    "row_wpe2": ["-DTCLB_FLAT_NODE=0", "-DTCLB_AD_WAVES=2"],
+                    "flat_wpe2": ["-DTCLB_AD_WAVES=2"]})
 
 
 def _variant_of(kind: str, variant: str) -> str:

@@ -154,8 +154,18 @@ __global__ void __launch_bounds__(256) k_rev(const Launch L) {
   }
 }
 
+// occupancy floor of k_ad (diagnostic build variants, -DTCLB_AD_WAVES=W): W = 2 keeps the
+// kernel within 256 registers (no AGPRs: spills go to scratch instead)
+#ifndef TCLB_AD_WAVES
+#define TCLB_AD_WAVES 0
+#endif
 template <class Model, int STG>
-__global__ void __launch_bounds__(AD_BLOCK) k_ad(const Launch L) {
+#if TCLB_AD_WAVES > 0
+__global__ void __launch_bounds__(AD_BLOCK) __attribute__((amdgpu_waves_per_eu(TCLB_AD_WAVES)))
+#else
+__global__ void __launch_bounds__(AD_BLOCK)
+#endif
+k_ad(const Launch L) {
   typedef Dual<double, TCLB_AD_WINDOW> D;
   constexpr int NG = Model::NGLOBALS_;
   constexpr int NSUM = Model::NSUMGLOBALS_;

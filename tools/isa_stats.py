@@ -75,11 +75,15 @@ def classify(op: str) -> str:
 def kernels(co: str):
     notes = subprocess.run([f"{LLVM}/llvm-readelf", "--notes", co], capture_output=True, text=True).stdout
     meta = {}
-    for blk in notes.split(".name:")[1:]:
-        name = blk.split("\n")[0].strip()
-        g = lambda k: int(m.group(1)) if (m := re.search(rf"\.{k}:\s*(\d+)", blk)) else -1  # noqa: E731
-        meta[name] = {"vgpr": g("vgpr_count"), "agpr": g("agpr_count"), "sgpr": g("sgpr_count"),
-                      "scratch": g("private_segment_fixed_size"), "lds": g("group_segment_fixed_size")}
+    # one YAML map per kernel, keys in alphabetical order: .agpr_count opens each entry
+    for blk in notes.split(".agpr_count:")[1:]:
+        m = re.search(r"\.name:\s*(\S+)", blk)
+        if not m:
+            continue
+        g = lambda k: int(m2.group(1)) if (m2 := re.search(rf"\.{k}:\s*(\d+)", blk)) else -1  # noqa: E731
+        agpr = int(blk.split("\n")[0].strip())
+        meta[m.group(1)] = {"vgpr": g("vgpr_count"), "agpr": agpr, "sgpr": g("sgpr_count"),
+                            "scratch": g("private_segment_fixed_size"), "lds": g("group_segment_fixed_size")}
     return meta
 
 
