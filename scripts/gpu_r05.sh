@@ -50,6 +50,7 @@ addiag) for v in default row_w2 row_w2_wpe2 row row_wpe2 flat_wpe2; do
           vv=$v; [ $v = default ] && vv=""
           step "adjoint diag $v" 300 $O/addiag_$v.jsonl env TCLB_AD_VARIANT=$vv python tools/adjoint_diag.py --repeats 2
         done ;;
+adbisect) step "row-form k_ad bisection" 900 $O/ad_bisect.jsonl python tools/ad_bisect.py check --limits ${LIMITS:-500,1000,2000,3000,4000,5000,6000,7000,8000,9000,10000,11000,12000,12696} ;;
 *) echo "unknown step $WHAT"; exit 2 ;;
 esac
 done

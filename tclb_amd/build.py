@@ -90,9 +90,24 @@ AD_VARIANTS.update({"row": ["-DTCLB_FLAT_NODE=0"], "row_o1": ["-DTCLB_FLAT_NODE=
                     "flat_wpe2": ["-DTCLB_AD_WAVES=2"]})
 
 
+def ad_variant_flags(variant: str) -> Optional[List[str]]:
+    """compile flags of an adjoint-executor variant: the named ones above, or
+    "<row|flat>_w<W>_bis<N>" — W tangents per pass and LLVM's optimisation bisection
+    stopped after pass N (-opt-bisect-limit, the pass search of the row-form k_ad
+    miscompile, tools/ad_bisect.py)"""
+    if variant in AD_VARIANTS:
+        return AD_VARIANTS[variant]
+    import re
+    m = re.fullmatch(r"(row|flat)_w(\d)_bis(\d+)", variant or "")
+    if not m:
+        return None
+    return ([] if m.group(1) == "flat" else ["-DTCLB_FLAT_NODE=0"]) + \
+        [f"-DTCLB_AD_WINDOW={m.group(2)}", "-mllvm", f"-opt-bisect-limit={m.group(3)}"]
+
+
 def _variant_of(kind: str, variant: str) -> str:
     """the variant a library of this kind is built in ("" for kinds without variants)"""
-    if kind == "hip" or (kind == "cpu" and variant in CPU_VARIANTS) or (kind == "adhip" and variant in AD_VARIANTS):
+    if kind == "hip" or (kind == "cpu" and variant in CPU_VARIANTS) or (kind == "adhip" and ad_variant_flags(variant) is not None):
         return variant
     return ""
 
@@ -181,7 +196,7 @@ def _cmd(kind: str, src: str, out: str, gen_dir: str, variant: str = "", model_f
     incs = ["-I", os.path.join(CSRC, "include"), "-I", os.path.join(CSRC, "models"), "-I", gen_dir]
     if kind == "adhip":
         return [HIPCC, f"--offload-arch={ARCH}", "-O2", "-std=c++17", "-fPIC", "-shared", "-munsafe-fp-atomics",
-                "-Wno-unused-result", "-Wno-pass-failed", *AD_VARIANTS.get(variant, []), *incs, src, "-o", out]
+                "-Wno-unused-result", "-Wno-pass-failed", *(ad_variant_flags(variant) or []), *incs, src, "-o", out]
     if kind == "hip":
         # simplifycfg-sink-common=false: boundary-condition switch cases that permute
         # the population array differ only in constant indices; sinking them into one

@@ -35,6 +35,7 @@ def one(dev, seeded: bool, reverse: bool, a_next_cpu):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--repeats", type=int, default=2)
+    ap.add_argument("--modes", default="all", help="all | dual (the dual-only step alone)")
     a = ap.parse_args()
     variant = os.environ.get("TCLB_AD_VARIANT", "")
     from test_gpu_adjoint import duct
@@ -42,8 +43,11 @@ def main():
     g = torch.Generator().manual_seed(11)
     a_next = torch.rand(ref_lat.snaps[0].shape, generator=g, dtype=torch.float64)
     bad_all = 0
-    for seeded, reverse, mode in ((True, False, "dual-only (seeded setting)"), (False, False, "dual-only"),
-                                  (False, True, "reverse + dual list")):
+    modes = ((True, False, "dual-only (seeded setting)"), (False, False, "dual-only"),
+             (False, True, "reverse + dual list"))
+    if a.modes == "dual":
+        modes = modes[1:2]
+    for seeded, reverse, mode in modes:
         lc, adc, ac = one("cpu", seeded, reverse, a_next)
         for rep in range(a.repeats):
             lg, adg, ag = one("cuda", seeded, reverse, a_next)
