@@ -60,7 +60,7 @@ def main():
         rows = [json.loads(ln) for ln in r.stdout.splitlines() if ln.startswith("{")]
         err = max((row["max_err"] for row in rows), default=None)
         print(json.dumps({"limit": n, "max_err": err, "bad_nodes": max((row["bad_nodes"] for row in rows), default=None),
-                          "rc": r.returncode, "stderr": r.stderr[-300:] if r.returncode not in (0, 1) else ""}),
+                          "rc": r.returncode, "stderr": r.stderr[-400:] if (r.returncode not in (0, 1) or not rows) else ""}),
               flush=True)
         if r.returncode not in (0, 1):
             break
