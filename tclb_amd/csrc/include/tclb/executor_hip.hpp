@@ -127,9 +127,12 @@ __device__ __forceinline__ uint3 tile_id(const Launch& L) {
   return make_uint3(b % gx, (b / gx) % gy, b / (gx * gy));
 }
 
-template <class Model, class R, class S, int STG, bool GLOB>
+// CLS: node class of a split stage (DSL add_stage(split=True), Node::node_class_): 1 / 2
+// run only the nodes of that class, each kernel compiled with that class's path alone;
+// 0 = every node (the stages that are not split)
+template <class Model, class R, class S, int STG, bool GLOB, int CLS = 0>
 __device__ __forceinline__ void stage_body(const Launch& L) {
-  typedef typename Model::template NodeT<R, S, GLOB> N;
+  typedef typename Model::template NodeCls<R, S, GLOB, CLS> N;
   typedef typename N::G_ G;   // fp64 accumulators, also in fp32-compute builds (core.hpp glob_acc)
   const uint3 t = tile_id(L);
   const int x = L.xlo + (int)(t.x * blockDim.x + threadIdx.x);
@@ -178,14 +181,14 @@ __device__ __forceinline__ void stage_body(const Launch& L) {
 #ifndef TCLB_STAGE_WAVES
 #define TCLB_STAGE_WAVES 0
 #endif
-template <class Model, class R, class S, int STG, bool GLOB>
+template <class Model, class R, class S, int STG, bool GLOB, int CLS = 0>
 #if TCLB_STAGE_WAVES > 0
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TCLB_STAGE_WAVES)))
 #else
 __global__ void __launch_bounds__(256)
 #endif
 k_stage(const Launch L) {
-  stage_body<Model, R, S, STG, GLOB>(L);
+  stage_body<Model, R, S, STG, GLOB, CLS>(L);
 }
 
 // Narrow-storage occupancy floor (build variant, -DTCLB_NARROW_WAVES=N): with fp32/fp16
@@ -212,9 +215,9 @@ k_stage_narrow(const Launch L) {
 template <class Model>
 constexpr int glob_waves() { return TCLB_GLOB_WAVES >= 0 ? TCLB_GLOB_WAVES : Model::GLOB_WAVES_; }
 
-template <class Model, class R, class S, int STG, int W>
+template <class Model, class R, class S, int STG, int W, int CLS = 0>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W))) k_stage_glob(const Launch L) {
-  stage_body<Model, R, S, STG, true>(L);
+  stage_body<Model, R, S, STG, true, CLS>(L);
 }
 
 // LDS-staged stencil tiles: csrc/include/tclb_tile/k_tile.hpp (a dependency of the
@@ -274,6 +277,17 @@ inline bool launch_one(const Launch& L, dim3 grid, dim3 block, hipStream_t s) {
     constexpr int ZC = Model::tile_zc(I);
     const dim3 tg((w + TILE_BX - 1) / TILE_BX, (h + TILE_BY - 1) / TILE_BY, (d + ZC - 1) / ZC);
     k_tile<Model, R, S, I, G><<<tg, dim3(TILE_BX, TILE_BY, 1), 0, s>>>(L);
+    return true;
+  }
+  if constexpr (Model::split_stage(I)) {
+    // one kernel per node class (the common interior path, then the rest)
+    if constexpr (G && glob_waves<Model>() > 0) {
+      k_stage_glob<Model, R, S, I, glob_waves<Model>(), 1><<<grid, block, 0, s>>>(L);
+      k_stage_glob<Model, R, S, I, glob_waves<Model>(), 2><<<grid, block, 0, s>>>(L);
+    } else {
+      k_stage<Model, R, S, I, G, 1><<<grid, block, 0, s>>>(L);
+      k_stage<Model, R, S, I, G, 2><<<grid, block, 0, s>>>(L);
+    }
     return true;
   }
   if constexpr (G && glob_waves<Model>() > 0) {

@@ -109,6 +109,9 @@ class Stage:
                               # load_<name>() where it needs them (declared for the halo)
     lds: Optional[List[str]] = None   # fields read through a stencil that the GPU kernel
                                       # stages in LDS tiles (executor_hip.hpp k_tile)
+    split: bool = False       # GPU: two kernels by node class (Node::node_class_(): 1 =
+                              # the common interior path, 2 = the rest), each compiled with
+                              # its own path only and so its own register budget
 
 
 @dataclass
@@ -278,14 +281,19 @@ class Model:
     def add_stage(self, name: str, main: Optional[str] = None, load_densities=False,
                   save_fields=False, read_fields: Optional[Sequence[str]] = None,
                   fixed_point: bool = False, particle: bool = False, init: bool = False,
-                  snapshot_reads: bool = False, lazy_load: bool = False, lds: Optional[Sequence[str]] = None):
+                  snapshot_reads: bool = False, lazy_load: bool = False, lds: Optional[Sequence[str]] = None,
+                  split: bool = False):
         """AddStage (src/conf.R:295-330): load_densities / save_fields are True (all), False
         (none) or lists of field names / group tags (reference defaults: FALSE).
         lazy_load: the stage's main pulls its densities itself (load_<name>()), e.g. only
         on the nodes a particle covers; the loads still count for halos and hazards.
         lds: fields (nicenames) the stage reads through a stencil, staged in LDS tiles by the
         GPU kernel (no reference counterpart: a MI355X schedule hint; the node code is
-        unchanged, the CPU and AD executors ignore it)."""
+        unchanged, the CPU and AD executors ignore it).
+        split: the GPU runs the stage as two kernels over the same box, one per node class
+        (the node code's node_class_(); NODE_CLASS is 1 / 2 in them, 0 in the executors
+        that run every node in one pass), so a rare heavy path (boundary closures) does not
+        set the register budget, and with it the occupancy, of the common one."""
         if save_fields is True:
             save_fields = None
         elif save_fields is False:
@@ -294,7 +302,7 @@ class Model:
                    save_fields=list(save_fields) if save_fields is not None else None,
                    read_fields=list(read_fields) if read_fields is not None else None,
                    fixed_point=fixed_point, particle=particle, init=init, snapshot_reads=snapshot_reads,
-                   lazy_load=lazy_load, lds=list(lds) if lds else None)
+                   lazy_load=lazy_load, lds=list(lds) if lds else None, split=split)
         self.stages = [s for s in self.stages if s.name != name] + [st]
         return st
 

@@ -146,7 +146,10 @@ def build(q27: bool = False, bgk: bool = False, thermo: bool = False, planarbenc
     m.add_stage("calcPhase", "calcPhaseF", save_fields=["PhaseF"], load_densities=load_phase, lazy_load=True)
     # (the collision's PhaseF stencil stays on global loads: an LDS tile of it made the
     # latency-bound collision 7-10 % slower, profiles/README.md r04a)
-    m.add_stage("BaseIter", "Run", save_fields=save_iteration, load_densities=load_iteration)
+    # lazy: Run pulls the populations where the interior MRT collision needs them; split:
+    # that path and the boundary closures run as two kernels (their own register budgets)
+    m.add_stage("BaseIter", "Run", save_fields=save_iteration, load_densities=load_iteration, lazy_load=True,
+                split=True)
     m.add_stage("InitFromFieldsStage", "InitFromFieldsStage", save_fields=save_initial_PF, load_densities=["init"])
     if geometric:           # Dynamics.R:129-135
         m.add_stage("WallInit_CA", "Init_wallNorm", save_fields=["nw", "solid_boundary"] + extra_bc)
@@ -318,6 +321,11 @@ def _field_index_block(m: Model) -> str:
         if idx:
             assert idx == list(range(idx[0], idx[0] + len(idx)))
             out.append(f"  static constexpr int FI_{arr.upper()}0 = {idx[0]};")
+    # the node-local values of the collision stage (d3q27_pf_velocity.inc Run, lazy pulls)
+    names = {f.name: i for i, f in enumerate(m.fields)}
+    for n in ("pnorm", "U", "V", "W", "nw_x", "nw_y", "nw_z", "IsSpecialBoundaryPoint"):
+        if n in names:
+            out.append(f"  static constexpr int FI_{n.upper()} = {names[n]};")
     return "\n".join(out)
 
 
