@@ -51,6 +51,22 @@ addiag) for v in default row_w2 row_w2_wpe2 row row_wpe2 flat_wpe2; do
           step "adjoint diag $v" 300 $O/addiag_$v.jsonl env TCLB_AD_VARIANT=$vv python tools/adjoint_diag.py --repeats 2
         done ;;
 adbisect) step "row-form k_ad bisection" 900 $O/ad_bisect.jsonl python tools/ad_bisect.py check --limits ${LIMITS:-500,1000,2000,3000,4000,5000,6000,7000,8000,9000,10000,11000,12000,12696} ;;
+splittests) step "split-stage model GPU tests" 600 $O/pytest_split.log python -u -m pytest tests -v -m gpu -k "pf_velocity or tePSM or split" --timeout 120 --timeout-method thread -p no:cacheprovider ;;
+splitperf) step "pf384 split A/B fp64" 600 $O/pf384_split_fp64.jsonl python tools/perf_models.py --models d3q27_pf_velocity --n3 384 --steps 20 --rounds 2 --variants ,cw3
+           step "pf384 split A/B mixed-shift" 600 $O/pf384_split_ms.jsonl python tools/perf_models.py --models d3q27_pf_velocity --n3 384 --steps 20 --rounds 2 --variants ,cw3 --precision mixed-shift
+           step "tePSM split A/B fp64" 600 $O/tepsm_split.jsonl python tools/perf_models.py --models d3q27_tePSM_per_NEBB --n3 256 --steps 20 --rounds 2 --variants ,cw2
+           step "bench_configs pf384 fp64" 600 $O/configs_pf384_fp64.jsonl python tools/bench_configs.py --configs pf384 --steps 100 --warmup 5
+           step "bench_configs pf384 mixed-shift" 600 $O/configs_pf384_ms.jsonl python tools/bench_configs.py --configs pf384 --steps 100 --warmup 5 --precision mixed-shift ;;
+splitab) step "pf384 split vs one kernel, mixed-shift" 600 $O/pf384_nosplit_ms.jsonl python tools/perf_models.py --models d3q27_pf_velocity --n3 384 --steps 20 --rounds 3 --variants ,nosplit --precision mixed-shift
+         step "pf384 split vs one kernel, fp64" 600 $O/pf384_nosplit_fp64.jsonl python tools/perf_models.py --models d3q27_pf_velocity --n3 384 --steps 20 --rounds 2 --variants ,nosplit
+         step "tePSM split vs one kernel" 600 $O/tepsm_nosplit.jsonl python tools/perf_models.py --models d3q27_tePSM_per_NEBB --n3 256 --steps 20 --rounds 3 --variants ,nosplit
+         step "pf thermo split vs one kernel" 600 $O/thermo_nosplit.jsonl python tools/perf_models.py --models d3q27_pf_velocity_thermo --n3 256 --steps 20 --rounds 2 --variants ,nosplit ;;
+pfconfigs) step "bench_configs pf384 fp64" 600 $O/configs_pf384_fp64.jsonl python tools/bench_configs.py --configs pf384 --steps 100 --warmup 5
+           step "bench_configs pf384 mixed-shift" 600 $O/configs_pf384_ms.jsonl python tools/bench_configs.py --configs pf384 --steps 100 --warmup 5 --precision mixed-shift ;;
+splitprof) export TMPDIR=/tmp
+           step "pf384 ms kernel trace" 300 $O/prof_pf384.log rocprofv3 --kernel-trace --stats -d $O/prof_pf384 -o run --output-format csv -- python3 tools/bench_configs.py --configs pf384 --steps 20 --warmup 3 --precision mixed-shift
+           step "tePSM kernel trace" 300 $O/prof_tepsm.log rocprofv3 --kernel-trace --stats -d $O/prof_tepsm -o run --output-format csv -- python3 tools/perf_models.py --models d3q27_tePSM_per_NEBB --n3 256 --steps 20 ;;
+heavy) step "heavy models 256^3 fp64" 900 $O/heavy_256.jsonl python tools/perf_models.py --models d3q27_tePSM_per_NEBB,d3q27q27_cm_cht,d3q27_pf_velocity_thermo,d3q19,d3q27_cumulant --n3 256 --steps 20 --rounds 2 ;;
 *) echo "unknown step $WHAT"; exit 2 ;;
 esac
 done

@@ -192,6 +192,7 @@ class Adjoint:
         L.zonal = lat.zonal_t.data_ptr()
         L.nzones = lat.zvals.shape[1]
         L.flags = lat.flags.data_ptr()
+        L.flags_gen = lat.flags_version
         L.in_ = inp.data_ptr()
         L.out = self.scratch.data_ptr()
         L.stage = si

@@ -56,6 +56,13 @@ VARIANTS = {
     # A/B of a 2-waves/SIMD floor on every stage kernel (executor_hip.hpp TCLB_STAGE_WAVES)
     "sw2": ["-DTCLB_NT_STORE=1", "-DTCLB_STAGE_WAVES=2"],
     "sw3": ["-DTCLB_NT_STORE=1", "-DTCLB_STAGE_WAVES=3"],
+    # node-class split stages (DSL add_stage(split=True)) as one kernel; a 2 / 3-waves/SIMD
+    # floor on the class-1 kernel of split stages only
+    "nosplit": ["-DTCLB_NT_STORE=1", "-DTCLB_NO_SPLIT=1"],
+    # class-2 kernels without their 2-wave floor (reproduces the r05m tePSM fault)
+    "c2w0": ["-DTCLB_NT_STORE=1", "-DTCLB_SPLIT_WAVES2=0"],
+    "cw2": ["-DTCLB_NT_STORE=1", "-DTCLB_SPLIT_WAVES=2"],
+    "cw3": ["-DTCLB_NT_STORE=1", "-DTCLB_SPLIT_WAVES=3"],
     # the round-2 form everywhere: flat accessors, register globals, no uniform-y hint
     # scheduler A/B: memory clauses grouped by the AMDGPU machine scheduler
     "mclause": ["-DTCLB_NT_STORE=1", "-mllvm", "-amdgpu-sched-strategy=max-memory-clause"],

@@ -97,7 +97,9 @@ struct Launch {
   // Tile windows (GPU): log2 of the number of contiguous tile ranges the work-groups are
   // dealt over (executor_hip.hpp tile_id); 0 = the hardware's linear block order
   int tile_split;
-  int reserved3;
+  // identity of the node types behind `flags` (process-unique, changed whenever they change:
+  // Lattice.flags_version); keys the per-class tile lists of split stages (executor_hip.hpp)
+  int flags_gen;
 };
 
 // Zonal-table read (reference ZoneSettings, one value per zone): the zone comes from the

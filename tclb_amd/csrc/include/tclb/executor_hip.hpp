@@ -10,7 +10,10 @@
 // (reference: per-warp(32) reduce + atomics, src/cuda.cu.Rt:93-179).
 #pragma once
 #include <hip/hip_runtime.h>
+#include <algorithm>
+#include <mutex>
 #include <utility>
+#include <vector>
 #include "core.hpp"
 
 namespace tclb {
@@ -131,10 +134,9 @@ __device__ __forceinline__ uint3 tile_id(const Launch& L) {
 // run only the nodes of that class, each kernel compiled with that class's path alone;
 // 0 = every node (the stages that are not split)
 template <class Model, class R, class S, int STG, bool GLOB, int CLS = 0>
-__device__ __forceinline__ void stage_body(const Launch& L) {
+__device__ __forceinline__ void stage_tile(const Launch& L, const uint3 t) {
   typedef typename Model::template NodeCls<R, S, GLOB, CLS> N;
   typedef typename N::G_ G;   // fp64 accumulators, also in fp32-compute builds (core.hpp glob_acc)
-  const uint3 t = tile_id(L);
   const int x = L.xlo + (int)(t.x * blockDim.x + threadIdx.x);
   // blockDim.x is a multiple of 64 (launch_shape), so a wave covers 64 x of one row:
   // y is wave-uniform.  In the row-form instantiations (N::ROWA_, the globals kernels)
@@ -173,6 +175,17 @@ __device__ __forceinline__ void stage_body(const Launch& L) {
       n.template run_stage<STG>();
     }
   }
+}
+template <class Model, class R, class S, int STG, bool GLOB, int CLS = 0>
+__device__ __forceinline__ void stage_body(const Launch& L) {
+  stage_tile<Model, R, S, STG, GLOB, CLS>(L, tile_id(L));
+}
+// a launch over a list of tiles (linear ids of the stage's tile grid, gx x gy x depth)
+__device__ __forceinline__ uint3 list_tile(const Launch& L, const unsigned* list, unsigned n, unsigned gx,
+                                           unsigned gy) {
+  const unsigned i = tile_linear(L, blockIdx.x, n);
+  const unsigned b = list ? list[i] : i;   // no list: every tile
+  return make_uint3(b % gx, (b / gx) % gy, b / (gx * gy));
 }
 
 // Occupancy floor of every stage kernel (build variant "sw2", -DTCLB_STAGE_WAVES=W): a
@@ -220,6 +233,137 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W))) k
   stage_body<Model, R, S, STG, true, CLS>(L);
 }
 
+// Occupancy floor of the class-1 kernel of a split stage (A/B knob, build variant flag
+// -DTCLB_SPLIT_WAVES=n; 0 = none)
+#ifndef TCLB_SPLIT_WAVES
+#define TCLB_SPLIT_WAVES 0
+#endif
+// A/B of the split itself (build variant nosplit): the stage as one kernel over all nodes
+#ifndef TCLB_NO_SPLIT
+#define TCLB_NO_SPLIT 0
+#endif
+template <class Model, class R, class S, int STG, bool GLOB, int W, int CLS>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W))) k_stage_w(const Launch L) {
+  stage_body<Model, R, S, STG, GLOB, CLS>(L);
+}
+
+// ---------------------------------------------------------------- class tile lists
+// A split stage runs one kernel per node class over the whole tile grid, each node skipping
+// the other class; the kernel of a class that holds no node of a tile still dispatches its
+// waves, at about 1 ns per wave for the chip: 1.07 ms of the 7.7 ms pf384 mixed-shift step
+// for a class-2 kernel with no class-2 node at all (profiles/README.md r05l).  So the
+// classes present in each tile are found once per node-type identity and launch geometry
+// (k_classify, Launch.flags_gen), and each class kernel runs over the list of its tiles
+// only (none: no launch; every tile: the plain grid).
+template <class Model, class R, class S>
+__global__ void __launch_bounds__(256) k_classify(const Launch L, unsigned char* out) {
+  typedef typename Model::template NodeCls<R, S, false, 1> N;
+  __shared__ int bits;
+  if (threadIdx.x == 0 && threadIdx.y == 0) bits = 0;
+  __syncthreads();
+  const int x = L.xlo + (int)(blockIdx.x * blockDim.x + threadIdx.x);
+  const int y = L.ylo + (int)(blockIdx.y * blockDim.y + threadIdx.y);
+  const int z = L.zlo + (int)blockIdx.z;
+  if (x < L.xhi && y < L.yhi) {
+    typename N::G_ g[1];
+    N n(L, x, y, z, g);
+    atomicOr(&bits, 1 << n.node_class_());
+  }
+  __syncthreads();
+  if (threadIdx.x == 0 && threadIdx.y == 0) out[blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z)] = (unsigned char)bits;
+}
+
+struct ClassTiles {
+  const void* flags;
+  int gen;
+  int box[6];
+  unsigned bx, by;
+  unsigned* list;   // device: the class-1 tiles, then the class-2 tiles
+  unsigned n1, n2, total;
+  unsigned long long used;
+};
+
+// the tile lists of this launch's geometry, built on first use (one synchronising classify
+// pass); nullptr if that failed (the caller then runs both classes over the full grid)
+template <class Model, class R, class S>
+inline const ClassTiles* class_tiles(const Launch& L, dim3 grid, dim3 block, hipStream_t s) {
+  static std::vector<ClassTiles> cache;
+  static std::mutex mu;
+  static unsigned long long clock = 0;
+  std::lock_guard<std::mutex> lk(mu);
+  const int box[6] = {L.xlo, L.xhi, L.ylo, L.yhi, L.zlo, L.zhi};
+  for (auto& c : cache) {
+    if (c.flags == L.flags && c.gen == L.flags_gen && c.bx == block.x && c.by == block.y &&
+        std::equal(box, box + 6, c.box)) {
+      c.used = ++clock;
+      return &c;
+    }
+  }
+  // entries of an older identity of these node types are stale; keep at most 32 others
+  for (size_t i = 0; i < cache.size();) {
+    if (cache[i].flags == L.flags && cache[i].gen != L.flags_gen) {
+      hipFree(cache[i].list);
+      cache.erase(cache.begin() + (long)i);
+    } else {
+      i++;
+    }
+  }
+  if (cache.size() >= 32) {
+    size_t o = 0;
+    for (size_t i = 1; i < cache.size(); i++)
+      if (cache[i].used < cache[o].used) o = i;
+    hipFree(cache[o].list);
+    cache.erase(cache.begin() + (long)o);
+  }
+  const unsigned total = grid.x * grid.y * grid.z;
+  unsigned char* d = nullptr;
+  if (hipMalloc(&d, total) != hipSuccess) return nullptr;
+  std::vector<unsigned char> h(total);
+  k_classify<Model, R, S><<<grid, block, 0, s>>>(L, d);
+  bool ok = hipGetLastError() == hipSuccess &&
+            hipMemcpyAsync(h.data(), d, total, hipMemcpyDeviceToHost, s) == hipSuccess &&
+            hipStreamSynchronize(s) == hipSuccess;
+  hipFree(d);
+  if (!ok) return nullptr;
+  std::vector<unsigned> l1, l2;
+  for (unsigned b = 0; b < total; b++) {
+    if (h[b] & 2) l1.push_back(b);
+    if (h[b] & 4) l2.push_back(b);
+  }
+  ClassTiles c;
+  c.flags = L.flags;
+  c.gen = L.flags_gen;
+  std::copy(box, box + 6, c.box);
+  c.bx = block.x;
+  c.by = block.y;
+  c.n1 = (unsigned)l1.size();
+  c.n2 = (unsigned)l2.size();
+  c.total = total;
+  c.used = ++clock;
+  c.list = nullptr;
+  l1.insert(l1.end(), l2.begin(), l2.end());
+  if (!l1.empty()) {
+    if (hipMalloc(&c.list, l1.size() * sizeof(unsigned)) != hipSuccess) return nullptr;
+    if (hipMemcpy(c.list, l1.data(), l1.size() * sizeof(unsigned), hipMemcpyHostToDevice) != hipSuccess) {
+      hipFree(c.list);
+      return nullptr;
+    }
+  }
+  cache.push_back(c);
+  return &cache.back();
+}
+
+template <class Model, class R, class S, int STG, bool GLOB, int CLS>
+__global__ void __launch_bounds__(256) k_stage_list(const Launch L, const unsigned* list, unsigned n, unsigned gx,
+                                                    unsigned gy) {
+  stage_tile<Model, R, S, STG, GLOB, CLS>(L, list_tile(L, list, n, gx, gy));
+}
+template <class Model, class R, class S, int STG, bool GLOB, int W, int CLS>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W)))
+k_stage_list_w(const Launch L, const unsigned* list, unsigned n, unsigned gx, unsigned gy) {
+  stage_tile<Model, R, S, STG, GLOB, CLS>(L, list_tile(L, list, n, gx, gy));
+}
+
 // LDS-staged stencil tiles: csrc/include/tclb_tile/k_tile.hpp (a dependency of the
 // libraries of models with LDS-staged stages only, build.py _tile_deps)
 #include "tclb_tile/k_tile.hpp"
@@ -258,9 +402,16 @@ inline void launch_shape(const Launch& L, dim3& grid, dim3& block, int sbytes = 
   // a multiple of 64: every wave is one row segment (stage_body's wave-uniform y)
   int bx = L.block_x > 0 ? (L.block_x + 63) / 64 * 64 : 0;
   if (bx == 0) {
+    // the widest row segment up to bmax that leaves the fewest idle lanes in the last
+    // x tile (384 wide, fp32 storage: 128 instead of 256, whose second tile is half idle)
     const int bmax = sbytes >= 8 ? 128 : 256;
-    bx = 64;
-    while (bx < bmax && bx < w) bx *= 2;
+    int best = 64;
+    for (int c = 64; c <= bmax; c *= 2) {
+      if (c > 64 && c >= 2 * w) break;
+      const int idle = (w + c - 1) / c * c - w, bidle = (w + best - 1) / best * best - w;
+      if (idle <= bidle) best = c;
+    }
+    bx = best;
   }
   if (bx > 256) bx = 256;
   int by = L.block_y > 0 ? L.block_y : 256 / bx;
@@ -268,6 +419,30 @@ inline void launch_shape(const Launch& L, dim3& grid, dim3& block, int sbytes = 
   if (bx * by > 256) by = 256 / bx;  // kernels are compiled with __launch_bounds__(256)
   block = dim3(bx, by, 1);
   grid = dim3((w + bx - 1) / bx, (h + by - 1) / by, d);
+}
+
+// Occupancy floor of the class-2 (boundary) kernels: 2 waves/SIMD, i.e. at most 256
+// VGPRs and no AGPRs.  Without it the d3q27_tePSM_per_NEBB class-2 tile-list kernel of the
+// plain (globals-free) step (344 registers, 88 of them AGPRs) stores wrong h populations on
+// wall nodes on the MI355X, while the same node code is right as the full-grid kernel, as
+// the globals kernel, with this floor, and on the CPU under UBSan (profiles/README.md
+// r05m; build variant c2w0 reproduces it).  The class-2 nodes are the few boundary ones,
+// so the spills of the floor cost nothing measurable.
+#ifndef TCLB_SPLIT_WAVES2
+#define TCLB_SPLIT_WAVES2 2
+#endif
+// one class of a split stage: over the list of its tiles (no class tiles: every tile)
+template <class Model, class R, class S, int I, bool G, int CLS>
+inline void launch_class(const Launch& L, dim3 grid, dim3 block, hipStream_t s, const ClassTiles* ct) {
+  constexpr int W = (G && glob_waves<Model>() > 0) ? glob_waves<Model>()
+                                                   : (CLS == 1 ? TCLB_SPLIT_WAVES : TCLB_SPLIT_WAVES2);
+  const unsigned n = !ct ? grid.x * grid.y * grid.z : (CLS == 1 ? ct->n1 : ct->n2);
+  if (n == 0) return;
+  // every tile: no list (the list entry is a dependent load at the start of each
+  // work-group, ~0.2 ms per step on the 1-wave tePSM collide)
+  const unsigned* list = (!ct || n == ct->total) ? nullptr : ct->list + (CLS == 1 ? 0 : ct->n1);
+  if constexpr (W > 0) k_stage_list_w<Model, R, S, I, G, W, CLS><<<dim3(n), block, 0, s>>>(L, list, n, grid.x, grid.y);
+  else k_stage_list<Model, R, S, I, G, CLS><<<dim3(n), block, 0, s>>>(L, list, n, grid.x, grid.y);
 }
 
 template <class Model, class R, class S, int I, bool G>
@@ -279,15 +454,12 @@ inline bool launch_one(const Launch& L, dim3 grid, dim3 block, hipStream_t s) {
     k_tile<Model, R, S, I, G><<<tg, dim3(TILE_BX, TILE_BY, 1), 0, s>>>(L);
     return true;
   }
-  if constexpr (Model::split_stage(I)) {
-    // one kernel per node class (the common interior path, then the rest)
-    if constexpr (G && glob_waves<Model>() > 0) {
-      k_stage_glob<Model, R, S, I, glob_waves<Model>(), 1><<<grid, block, 0, s>>>(L);
-      k_stage_glob<Model, R, S, I, glob_waves<Model>(), 2><<<grid, block, 0, s>>>(L);
-    } else {
-      k_stage<Model, R, S, I, G, 1><<<grid, block, 0, s>>>(L);
-      k_stage<Model, R, S, I, G, 2><<<grid, block, 0, s>>>(L);
-    }
+  if constexpr (Model::split_stage(I) && !TCLB_NO_SPLIT) {
+    // one kernel per node class (the common interior path, then the rest), each over the
+    // tiles that hold nodes of its class
+    const ClassTiles* ct = class_tiles<Model, R, S>(L, grid, block, s);
+    launch_class<Model, R, S, I, G, 1>(L, grid, block, s, ct);
+    launch_class<Model, R, S, I, G, 2>(L, grid, block, s, ct);
     return true;
   }
   if constexpr (G && glob_waves<Model>() > 0) {

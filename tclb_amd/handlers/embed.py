@@ -324,7 +324,7 @@ def _refresh_flag_ghosts(lat):
     else:
         v = torch.where(v >= 1 << 31, v - (1 << 32), v)
     lat.flags.copy_(v.to(lat.flags.dtype))
-    lat.flags_version += 1
+    lat.flags_changed()
 
 
 class Parameters(_Obj):

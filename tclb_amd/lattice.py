@@ -33,6 +33,8 @@ from .parallel.decomp import Slab, decompose
 from .parallel.native import NativeLoop, native_dist_enabled
 from .utils import trace
 
+_FLAGS_GEN = iter(range(1, 2 ** 31 - 1))      # process-unique node-type identities
+
 _SAFE_MATH = {k: getattr(math, k) for k in ("sqrt", "exp", "log", "sin", "cos", "tan", "atan", "atan2", "pi",
                                               "pow", "fabs", "floor", "ceil", "tanh", "sinh", "cosh", "acos", "asin")}
 _SAFE_MATH["abs"] = abs
@@ -126,7 +128,10 @@ class Lattice:
         self.cur = 0
         fdt = torch.int16 if m.flag_bits == 16 else torch.int32
         self.flags = torch.zeros((self.NZ, self.NY, self.px), dtype=fdt, device=self.device)
-        self.flags_version = 0            # bumped by every set_flags (caches keyed on the node types)
+        # identity of the node types, process-unique and renewed by every change
+        # (flags_changed): keys caches of the node types (the adjoint's dual flags, the GPU
+        # executor's class tile lists of split stages, Launch.flags_gen)
+        self.flags_version = next(_FLAGS_GEN)
         # settings
         self.gsettings = [s.name for s in m.global_settings]
         self.zsettings = [s.name for s in m.zonal_settings]
@@ -269,6 +274,7 @@ class Lattice:
         L.xlo, L.xhi, L.ylo, L.yhi, L.zlo, L.zhi = 0, nx, 0, ny, 0, nz
         L.block_x, L.block_y = self.block
         L.flags = self.flags.data_ptr()
+        L.flags_gen = self.flags_version
         L.storage_shift = 1 if self.storage_shift else 0
         L.tile_split = self.tile_split
         return L
@@ -288,6 +294,7 @@ class Lattice:
         L.nzones = self.zvals.shape[1]
         L.globals_ = self.globals_t.data_ptr()
         L.flags = self.flags.data_ptr()
+        L.flags_gen = self.flags_version
         if self.turb_t is not None:
             L.ext[0] = self.turb_t.data_ptr()
             L.next[0] = self.turb_t.shape[0]
@@ -866,7 +873,11 @@ class Lattice:
         full[:, :, :nx] = flags
         view = full.view(np.int16 if self.model.flag_bits == 16 else np.int32)
         self.flags.copy_(torch.from_numpy(view))
-        self.flags_version += 1
+        self.flags_changed()
+
+    def flags_changed(self):
+        """to be called after any write into self.flags"""
+        self.flags_version = next(_FLAGS_GEN)
 
     def get_flags(self) -> np.ndarray:
         """interior flags (nz, ny, nx) as unsigned"""

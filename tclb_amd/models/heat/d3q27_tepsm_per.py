@@ -84,8 +84,10 @@ def build(nebb: bool = False, sup: bool = False, isothermal: bool = False) -> Mo
         calc_load = ["f", "Force", "l"]
     # the initial coverage (CalcPeriodicSolid in Init) needs the particles: particle stage
     m.add_stage("BaseInit", "Init", save_fields=groups, load_densities=groups, particle=True)
-    m.add_stage("BaseIteration", "Run", save_fields=groups, load_densities=groups)
-    m.add_stage("CalcF", "CalcF", save_fields=["Force"], load_densities=calc_load, particle=True)
+    # split: the interior collision and the face closures run as two kernels
+    m.add_stage("BaseIteration", "Run", save_fields=groups, load_densities=groups, split=True)
+    # lazy: the populations are pulled only where a particle covers the node
+    m.add_stage("CalcF", "CalcF", save_fields=["Force"], load_densities=calc_load, particle=True, lazy_load=True)
     m.add_action("Iteration", ["BaseIteration", "CalcF"])
     m.add_action("Init", ["BaseInit", "CalcF"])
     m.add_node_type("Solid", "BOUNDARY")

@@ -149,7 +149,7 @@ def build(q27: bool = False, bgk: bool = False, thermo: bool = False, planarbenc
     # lazy: Run pulls the populations where the interior MRT collision needs them; split:
     # that path and the boundary closures run as two kernels (their own register budgets)
     m.add_stage("BaseIter", "Run", save_fields=save_iteration, load_densities=load_iteration, lazy_load=True,
-                split=True)
+                split=not (bgk or outflow or autosym or staircaseimp))   # = PF_LAZY_INTERIOR
     m.add_stage("InitFromFieldsStage", "InitFromFieldsStage", save_fields=save_initial_PF, load_densities=["init"])
     if geometric:           # Dynamics.R:129-135
         m.add_stage("WallInit_CA", "Init_wallNorm", save_fields=["nw", "solid_boundary"] + extra_bc)

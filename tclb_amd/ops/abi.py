@@ -71,7 +71,8 @@ class Launch(ctypes.Structure):
         ("mslot", ctypes.c_byte * MIRROR_FIELDS),
         # log2 of the tile windows of the GPU block -> tile map (executor_hip.hpp tile_id)
         ("tile_split", ctypes.c_int),
-        ("reserved3", ctypes.c_int),
+        # identity of the node types (Lattice.flags_version; executor_hip.hpp class tile lists)
+        ("flags_gen", ctypes.c_int),
     ]
 
 

@@ -56,7 +56,7 @@ def collision_check(lat, action: str = "Iteration", min_rel: float = 1e-12) -> D
                 lat.snaps[1 - cur].copy_(other)
             lat.cur, lat.iter = cur, it
             lat.flags.copy_(flags & keep if clear else flags)
-            lat.flags_version += 1
+            lat.flags_changed()
             lat.iterate(1, glob_last=False, action=action)
             res = lat.snaps[lat.cur][:, lat.gz:lat.gz + nz, lat.gy:lat.gy + ny, :nx]
             if first is None:
@@ -71,7 +71,7 @@ def collision_check(lat, action: str = "Iteration", min_rel: float = 1e-12) -> D
     finally:
         lat.particles = ps
         lat.flags.copy_(flags)
-        lat.flags_version += 1
+        lat.flags_changed()
         lat.snaps[cur].copy_(state)
         if other is not None:
             lat.snaps[1 - cur].copy_(other)

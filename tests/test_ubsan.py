@@ -35,7 +35,8 @@ print("ok", name)
 
 
 @pytest.mark.parametrize("name,shape", [("d2q9", "16,8,1"), ("d3q27", "8,6,4"), ("d2q9_kuper", "12,8,1"),
-                                        ("d3q27_cumulant", "6,6,4")])
+                                        ("d3q27_cumulant", "6,6,4"),
+                                        ("d3q27_tePSM_per_NEBB", "8,6,4"), ("d3q27_pf_velocity", "8,6,4")])
 def test_model_under_ubsan(name, shape):
     env = dict(os.environ, UBSAN_OPTIONS="halt_on_error=1:print_stacktrace=1", OMP_NUM_THREADS="2")
     r = subprocess.run([sys.executable, "-c", SCRIPT, name, shape], cwd=ROOT, env=env, capture_output=True,

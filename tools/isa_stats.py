@@ -137,7 +137,8 @@ def main():
             if not targs or f", {a.stage}, " not in targs.group(1):
                 continue
         mt, c = meta[n], dis.get(n.replace(".kd", ""), Counter())
-        regs = max(1, mt["vgpr"] + max(0, mt["agpr"]))
+        # .vgpr_count is the unified file (arch VGPRs + AGPRs, e.g. 344 = 256 + 88)
+        regs = max(1, mt["vgpr"])
         waves = min(8, 512 // ((regs + 7) // 8 * 8))
         valu = sum(v for k, v in c.items() if k.startswith("valu"))
         short = d if len(d) < 140 else d[:137] + "..."
