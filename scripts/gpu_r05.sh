@@ -67,6 +67,10 @@ splitprof) export TMPDIR=/tmp
            step "pf384 ms kernel trace" 300 $O/prof_pf384.log rocprofv3 --kernel-trace --stats -d $O/prof_pf384 -o run --output-format csv -- python3 tools/bench_configs.py --configs pf384 --steps 20 --warmup 3 --precision mixed-shift
            step "tePSM kernel trace" 300 $O/prof_tepsm.log rocprofv3 --kernel-trace --stats -d $O/prof_tepsm -o run --output-format csv -- python3 tools/perf_models.py --models d3q27_tePSM_per_NEBB --n3 256 --steps 20 ;;
 heavy) step "heavy models 256^3 fp64" 900 $O/heavy_256.jsonl python tools/perf_models.py --models d3q27_tePSM_per_NEBB,d3q27q27_cm_cht,d3q27_pf_velocity_thermo,d3q19,d3q27_cumulant --n3 256 --steps 20 --rounds 2 ;;
+heavycounters) export TMPDIR=/tmp
+           step "tePSM counters" 600 $O/ctr_tepsm.log python tools/counters.py --tag tepsm_256 --outdir $O/counters --nodes 16777216 --passes 0,1,2,3 -- python3 tools/perf_models.py --models d3q27_tePSM_per_NEBB --n3 256 --steps 5
+           step "thermo counters" 600 $O/ctr_thermo.log python tools/counters.py --tag thermo_256 --outdir $O/counters --nodes 16777216 --passes 0,1,2,3 -- python3 tools/perf_models.py --models d3q27_pf_velocity_thermo --n3 256 --steps 5
+           step "pf384 fp64 counters" 600 $O/ctr_pf384.log python tools/counters.py --tag pf384_fp64 --outdir $O/counters --nodes 56623104 --passes 0,1,2,3 -- python3 tools/bench_configs.py --configs pf384 --steps 5 --warmup 1 ;;
 *) echo "unknown step $WHAT"; exit 2 ;;
 esac
 done

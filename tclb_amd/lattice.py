@@ -132,6 +132,8 @@ class Lattice:
         # (flags_changed): keys caches of the node types (the adjoint's dual flags, the GPU
         # executor's class tile lists of split stages, Launch.flags_gen)
         self.flags_version = next(_FLAGS_GEN)
+        self._kept_cache: Dict[str, List[int]] = {}
+        self._iterating = False
         # settings
         self.gsettings = [s.name for s in m.global_settings]
         self.zsettings = [s.name for s in m.zonal_settings]
@@ -575,6 +577,8 @@ class Lattice:
         act = m.action(name)
         if act is None:
             raise KeyError(f"model {m.name} has no action {name}")
+        if not self._iterating:
+            self._mirror_kept(name)
         self._sync_settings()
         src = self.snaps[self.cur]
         dst = self.snaps[1 - self.cur]
@@ -716,6 +720,7 @@ class Lattice:
         samplers)."""
         if n <= 0:
             return
+        self._mirror_kept(action)
         path = self._native_path(action)
         if path is not None:
             m = self.model
@@ -763,16 +768,45 @@ class Lattice:
                     self._dist.wait()
                 self._reduce_globals()
             return
-        for i in range(n):
-            glob = glob_last and i == n - 1
-            if self.zseries:
-                self.apply_series()
-            self.run_action(action, glob=glob, reduce=reduce)
-            self.iter += 1
-            for smp in self.samplers:
-                smp.sample_now()
-            for cb in self.callbacks:
-                cb(self)
+        self._iterating = True
+        try:
+            for i in range(n):
+                glob = glob_last and i == n - 1
+                if self.zseries:
+                    self.apply_series()
+                self.run_action(action, glob=glob, reduce=reduce)
+                self.iter += 1
+                for smp in self.samplers:
+                    smp.sample_now()
+                for cb in self.callbacks:
+                    cb(self)
+        finally:
+            self._iterating = False
+
+    def _kept_fields(self, action: str) -> List[int]:
+        """indices of the fields that a stage of `action` keeps (DSL add_stage(keep=...)):
+        unchanged by it and not stored, so both snapshots must hold them"""
+        c = self._kept_cache.get(action)
+        if c is None:
+            m = self.model
+            act = m.action(action)
+            tags = [t for s in (act.stages if act else []) for t in (m.stage(s).keep or [])]
+            c = [i for i, f in enumerate(m.fields) if tags and m.matches(f, tags)]
+            self._kept_cache[action] = c
+        return c
+
+    def _mirror_kept(self, action: str):
+        """copy the kept fields of `action` (whole planes, ghosts included) from the current
+        snapshot into the other one: whatever wrote them last (an initialisation stage, a
+        field load, a checkpoint restore) wrote one snapshot; the action's steps alternate
+        between the two and never store them.  A device copy of a few fields per iterate
+        call, against a read and a write of each of them per node and step."""
+        idx = self._kept_fields(action)
+        if not idx:
+            return
+        src, dst = self.snaps[self.cur], self.snaps[1 - self.cur]
+        for i in idx:
+            dst[i].copy_(src[i])
 
     # ------------------------------------------------------------------ settings
     def set_setting(self, name: str, value: float, zone: Optional[str] = None, _init: bool = False):

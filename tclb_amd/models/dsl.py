@@ -112,6 +112,9 @@ class Stage:
     split: bool = False       # GPU: two kernels by node class (Node::node_class_(): 1 =
                               # the common interior path, 2 = the rest), each compiled with
                               # its own path only and so its own register budget
+    keep: Optional[List[str]] = None   # fields (nicenames / group tags) the stage leaves
+                                       # unchanged and does not store; the lattice keeps
+                                       # both snapshots' copies equal (Lattice._mirror_kept)
 
 
 @dataclass
@@ -282,7 +285,7 @@ class Model:
                   save_fields=False, read_fields: Optional[Sequence[str]] = None,
                   fixed_point: bool = False, particle: bool = False, init: bool = False,
                   snapshot_reads: bool = False, lazy_load: bool = False, lds: Optional[Sequence[str]] = None,
-                  split: bool = False):
+                  split: bool = False, keep: Optional[Sequence[str]] = None):
         """AddStage (src/conf.R:295-330): load_densities / save_fields are True (all), False
         (none) or lists of field names / group tags (reference defaults: FALSE).
         lazy_load: the stage's main pulls its densities itself (load_<name>()), e.g. only
@@ -291,18 +294,29 @@ class Model:
         GPU kernel (no reference counterpart: a MI355X schedule hint; the node code is
         unchanged, the CPU and AD executors ignore it).
         split: the GPU runs the stage as two kernels over the same box, one per node class
-        (the node code's node_class_(); NODE_CLASS is 1 / 2 in them, 0 in the executors
-        that run every node in one pass), so a rare heavy path (boundary closures) does not
-        set the register budget, and with it the occupancy, of the common one."""
+        (the node code's node_class_(); its CLS_ template argument is 1 / 2 in them, 0 in
+        the executors that run every node in one pass), so a rare heavy path (boundary
+        closures) does not set the register budget, and with it the occupancy, of the
+        common one.
+        keep: entries of save_fields (same tags) that the stage never changes, e.g. wall
+        normals set at initialisation: they are not stored (no read and write of them per
+        node and step) and the lattice copies them into the other snapshot once before an
+        action that has such a stage runs (no reference counterpart: TCLB stores every
+        declared field in every step)."""
         if save_fields is True:
             save_fields = None
         elif save_fields is False:
             save_fields = []
+        if keep:
+            if save_fields is None or any(k not in save_fields for k in keep):
+                raise ModelError(f"stage {name}: keep entries must be entries of an explicit save_fields list")
+            save_fields = [x for x in save_fields if x not in keep]
         st = Stage(name=name, main=main or name, load_densities=load_densities,
                    save_fields=list(save_fields) if save_fields is not None else None,
                    read_fields=list(read_fields) if read_fields is not None else None,
                    fixed_point=fixed_point, particle=particle, init=init, snapshot_reads=snapshot_reads,
-                   lazy_load=lazy_load, lds=list(lds) if lds else None, split=split)
+                   lazy_load=lazy_load, lds=list(lds) if lds else None, split=split,
+                   keep=list(keep) if keep else None)
         self.stages = [s for s in self.stages if s.name != name] + [st]
         return st
 

@@ -148,8 +148,11 @@ def build(q27: bool = False, bgk: bool = False, thermo: bool = False, planarbenc
     # latency-bound collision 7-10 % slower, profiles/README.md r04a)
     # lazy: Run pulls the populations where the interior MRT collision needs them; split:
     # that path and the boundary closures run as two kernels (their own register budgets)
+    # keep: the wall normals and boundary markers are set by the wall-init stages only
+    # (Init_wallNorm); the collision reads them where it needs them and never stores them
     m.add_stage("BaseIter", "Run", save_fields=save_iteration, load_densities=load_iteration, lazy_load=True,
-                split=not (bgk or outflow or autosym or staircaseimp))   # = PF_LAZY_INTERIOR
+                split=not (bgk or outflow or autosym or staircaseimp),   # = PF_LAZY_INTERIOR
+                keep=["nw", "solid_boundary"])
     m.add_stage("InitFromFieldsStage", "InitFromFieldsStage", save_fields=save_initial_PF, load_densities=["init"])
     if geometric:           # Dynamics.R:129-135
         m.add_stage("WallInit_CA", "Init_wallNorm", save_fields=["nw", "solid_boundary"] + extra_bc)

@@ -1,0 +1,61 @@
+"""Fields a stage keeps (DSL add_stage(keep=...)): d3q27_pf_velocity's collision no longer
+stores the wall normals and boundary markers (set by the wall-init stages only), and the
+lattice copies them into the other snapshot before an action with such a stage runs
+(Lattice._mirror_kept).  The fixture holds per-field sums of the same case run by the
+build that still stored them (every field of the current snapshot after an odd number of
+steps, so the mirror is needed for them to be right)."""
+import json
+import os
+
+import pytest
+import torch
+
+from model_cases import make_case, perturb
+from tclb_amd.lattice import Lattice
+from tclb_amd.models import registry
+from tclb_amd.models.dsl import Model, ModelError
+
+REF = os.path.join(os.path.dirname(__file__), "data", "pf_velocity_keep_ref.json")
+
+
+def test_keep_declaration():
+    st = registry.get("d3q27_pf_velocity").stage("BaseIter")
+    assert st.keep == ["nw", "solid_boundary"]
+    assert "nw" not in st.save_fields and "solid_boundary" not in st.save_fields
+    m = Model("k", dims=2)
+    with pytest.raises(ModelError):
+        m.add_stage("S", save_fields=True, keep=["x"])
+    with pytest.raises(ModelError):
+        m.add_stage("S", save_fields=["a"], keep=["b"])
+
+
+def _run():
+    lat = make_case("d3q27_pf_velocity", "cpu")
+    lat.init()
+    perturb(lat)
+    lat.iterate(3)
+    return lat
+
+
+def test_kept_fields_match_storing_build():
+    lat = _run()
+    a = lat.fields_interior().double()
+    ref = json.load(open(REF))
+    for i in range(a.shape[0]):
+        for key, v in (("sum", float(a[i].sum())), ("l2", float(a[i].pow(2).sum().sqrt()))):
+            r = ref[key][i]
+            assert abs(v - r) <= 1e-12 * max(1.0, abs(r)), (lat.model.fields[i].name, key, v, r)
+    idx = lat._kept_fields("Iteration")
+    assert [lat.model.fields[i].name for i in idx] == ["nw_x", "nw_y", "nw_z", "IsSpecialBoundaryPoint",
+                                                       "IsBoundary"]
+    assert float(a[idx].abs().max()) > 0.5            # the case has wall normals
+    # both snapshots hold them
+    assert torch.equal(lat.snaps[0][idx], lat.snaps[1][idx])
+
+
+def test_mirror_is_needed(monkeypatch):
+    """without the mirror the other snapshot has no normals: wrong after an odd step count"""
+    good = _run().fields_interior().clone()
+    monkeypatch.setattr(Lattice, "_mirror_kept", lambda self, action: None)
+    bad = _run().fields_interior()
+    assert not torch.equal(good, bad)
