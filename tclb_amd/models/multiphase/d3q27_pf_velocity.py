@@ -139,7 +139,10 @@ def build(q27: bool = False, bgk: bool = False, thermo: bool = False, planarbenc
     if thermo:
         _thermo_declarations(m, planarbenchmark)
         save_initial_PF = save_initial_PF + ["Thermal"]
-        save_iteration += ["Thermal"]
+        # the collision stores the temperature and surface tension that the RK stages of
+        # the same step read; it keeps (does not store) the conductivity, set at
+        # initialisation only, and the RK iterates, which the RK stages rewrite before any read
+        save_iteration += ["Temp", "SurfaceTension", "Cond", "RK1", "RK2", "RK3"]
         load_iteration += ["Thermal"]
     m.add_stage("PhaseInit", "Init", save_fields=save_initial_PF)
     m.add_stage("BaseInit", "Init_distributions", save_fields=save_initial)
@@ -152,7 +155,7 @@ def build(q27: bool = False, bgk: bool = False, thermo: bool = False, planarbenc
     # (Init_wallNorm); the collision reads them where it needs them and never stores them
     m.add_stage("BaseIter", "Run", save_fields=save_iteration, load_densities=load_iteration, lazy_load=True,
                 split=not (bgk or outflow or autosym or staircaseimp),   # = PF_LAZY_INTERIOR
-                keep=["nw", "solid_boundary"])
+                keep=["nw", "solid_boundary"] + (["Cond", "RK1", "RK2", "RK3"] if thermo else []))
     m.add_stage("InitFromFieldsStage", "InitFromFieldsStage", save_fields=save_initial_PF, load_densities=["init"])
     if geometric:           # Dynamics.R:129-135
         m.add_stage("WallInit_CA", "Init_wallNorm", save_fields=["nw", "solid_boundary"] + extra_bc)

@@ -59,3 +59,21 @@ def test_mirror_is_needed(monkeypatch):
     monkeypatch.setattr(Lattice, "_mirror_kept", lambda self, action: None)
     bad = _run().fields_interior()
     assert not torch.equal(good, bad)
+
+
+def test_thermo_kept_fields_match_storing_build():
+    """pf_velocity_thermo also keeps the conductivity and the RK iterates (rewritten by the
+    RK stages of the same step before any read); the constant-temperature action too"""
+    ref = json.load(open(REF))
+    lat = make_case("d3q27_pf_velocity_thermo", "cpu")
+    lat.init()
+    perturb(lat)
+    lat.iterate(3)
+    for key, act in (("d3q27_pf_velocity_thermo", None), ("d3q27_pf_velocity_thermo_ct", "IterationConstantTemp")):
+        if act:
+            lat.iterate(2, action=act)
+        a = lat.fields_interior().double()
+        for i in range(a.shape[0]):
+            for k, v in (("sum", float(a[i].sum())), ("l2", float(a[i].pow(2).sum().sqrt()))):
+                r = ref[key][k][i]
+                assert abs(v - r) <= 1e-12 * max(1.0, abs(r)), (key, lat.model.fields[i].name, k, v, r)
