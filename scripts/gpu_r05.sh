@@ -51,7 +51,7 @@ addiag) for v in default row_w2 row_w2_wpe2 row row_wpe2 flat_wpe2; do
           step "adjoint diag $v" 300 $O/addiag_$v.jsonl env TCLB_AD_VARIANT=$vv python tools/adjoint_diag.py --repeats 2
         done ;;
 adbisect) step "row-form k_ad bisection" 900 $O/ad_bisect.jsonl python tools/ad_bisect.py check --limits ${LIMITS:-500,1000,2000,3000,4000,5000,6000,7000,8000,9000,10000,11000,12000,12696} ;;
-splittests) step "split-stage model GPU tests" 600 $O/pytest_split.log python -u -m pytest tests -v -m gpu -k "pf_velocity or tePSM or split" --timeout 120 --timeout-method thread -p no:cacheprovider ;;
+splittests) step "split-stage model GPU tests" 600 $O/pytest_split.log python -u -m pytest tests -v -m gpu -k "pf_velocity or tePSM or split or kept" --timeout 120 --timeout-method thread -p no:cacheprovider ;;
 splitperf) step "pf384 split A/B fp64" 600 $O/pf384_split_fp64.jsonl python tools/perf_models.py --models d3q27_pf_velocity --n3 384 --steps 20 --rounds 2 --variants ,cw3
            step "pf384 split A/B mixed-shift" 600 $O/pf384_split_ms.jsonl python tools/perf_models.py --models d3q27_pf_velocity --n3 384 --steps 20 --rounds 2 --variants ,cw3 --precision mixed-shift
            step "tePSM split A/B fp64" 600 $O/tepsm_split.jsonl python tools/perf_models.py --models d3q27_tePSM_per_NEBB --n3 256 --steps 20 --rounds 2 --variants ,cw2

@@ -255,7 +255,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W))) k
 // classes present in each tile are found once per node-type identity and launch geometry
 // (k_classify, Launch.flags_gen), and each class kernel runs over the list of its tiles
 // only (none: no launch; every tile: the plain grid).
-template <class Model, class R, class S>
+template <class Model, class R, class S, int STG>
 __global__ void __launch_bounds__(256) k_classify(const Launch L, unsigned char* out) {
   typedef typename Model::template NodeCls<R, S, false, 1> N;
   __shared__ int bits;
@@ -267,7 +267,7 @@ __global__ void __launch_bounds__(256) k_classify(const Launch L, unsigned char*
   if (x < L.xhi && y < L.yhi) {
     typename N::G_ g[1];
     N n(L, x, y, z, g);
-    atomicOr(&bits, 1 << n.node_class_());
+    atomicOr(&bits, 1 << n.node_class_(STG));   // class 0: no work in this stage
   }
   __syncthreads();
   if (threadIdx.x == 0 && threadIdx.y == 0) out[blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z)] = (unsigned char)bits;
@@ -284,8 +284,9 @@ struct ClassTiles {
 };
 
 // the tile lists of this launch's geometry, built on first use (one synchronising classify
-// pass); nullptr if that failed (the caller then runs both classes over the full grid)
-template <class Model, class R, class S>
+// pass); nullptr if that failed (the caller then runs both classes over the full grid).
+// Node::node_class_(stage): 1, 2, or 0 for a node the stage leaves alone (on no list)
+template <class Model, class R, class S, int STG>
 inline const ClassTiles* class_tiles(const Launch& L, dim3 grid, dim3 block, hipStream_t s) {
   static std::vector<ClassTiles> cache;
   static std::mutex mu;
@@ -319,7 +320,7 @@ inline const ClassTiles* class_tiles(const Launch& L, dim3 grid, dim3 block, hip
   unsigned char* d = nullptr;
   if (hipMalloc(&d, total) != hipSuccess) return nullptr;
   std::vector<unsigned char> h(total);
-  k_classify<Model, R, S><<<grid, block, 0, s>>>(L, d);
+  k_classify<Model, R, S, STG><<<grid, block, 0, s>>>(L, d);
   bool ok = hipGetLastError() == hipSuccess &&
             hipMemcpyAsync(h.data(), d, total, hipMemcpyDeviceToHost, s) == hipSuccess &&
             hipStreamSynchronize(s) == hipSuccess;
@@ -457,7 +458,7 @@ inline bool launch_one(const Launch& L, dim3 grid, dim3 block, hipStream_t s) {
   if constexpr (Model::split_stage(I) && !TCLB_NO_SPLIT) {
     // one kernel per node class (the common interior path, then the rest), each over the
     // tiles that hold nodes of its class
-    const ClassTiles* ct = class_tiles<Model, R, S>(L, grid, block, s);
+    const ClassTiles* ct = class_tiles<Model, R, S, I>(L, grid, block, s);
     launch_class<Model, R, S, I, G, 1>(L, grid, block, s, ct);
     launch_class<Model, R, S, I, G, 2>(L, grid, block, s, ct);
     return true;

@@ -189,7 +189,9 @@ def build(q27: bool = False, bgk: bool = False, thermo: bool = False, planarbenc
                     load_densities=["U", "V", "W", "RK1", "RK2", "Cond", "Temp"], lds=["RK2", "Cond"])
         m.add_stage("RK_4", "TempUpdate4", save_fields=["Temp", "SurfaceTension"],
                     load_densities=["U", "V", "W", "RK1", "RK2", "RK3", "Cond", "Temp"], lds=["RK3", "Cond"])
-        m.add_stage("NonLocalTemp", "BoundUpdate", save_fields=["Temp", "SurfaceTension"], load_densities=["Temp"])
+        # split: on the GPU the stage runs on the EAdiabatic nodes only (node_class_)
+        m.add_stage("NonLocalTemp", "BoundUpdate", save_fields=["Temp", "SurfaceTension"], load_densities=["Temp"],
+                    split=True)
         rk = ["RK_1", "RK_2", "RK_3", "RK_4", "NonLocalTemp"]
         m.add_action("TempToSteadyState", ["CopyDistributions"] + rk)
         m.add_action("Iteration", ["BaseIter", "calcPhase", "calcWall"] + rk)

@@ -100,3 +100,27 @@ def test_split_reused_flag_buffer():
     fa, fb = res
     scale = fb.abs().max().item()
     assert torch.allclose(fa, fb, atol=1e-11 * scale, rtol=1e-11), ((fa - fb).abs().max().item(), reused)
+
+
+@pytest.mark.gpu
+@needs_gpu
+def test_thermo_nonlocaltemp_adiabatic_nodes():
+    """pf_velocity_thermo's NonLocalTemp is split with class 0 (no work) for every node but
+    the EAdiabatic ones; a plane of those must come out as on the CPU, which runs the
+    stage on every node"""
+    name = "d3q27_pf_velocity_thermo"
+    out = []
+    for dev in ("cuda", "cpu"):
+        lat = make_case(name, dev, shape=(40, 16, 12))
+        m = lat.model
+        nx = lat.shape[0]
+        full = lat.flags.cpu().numpy().view(np.uint16 if m.flag_bits == 16 else np.uint32)[:, :, :nx].copy()
+        full[:, :, 20] |= m.node_type("EAdiabatic").value
+        lat.set_flags(full)
+        lat.init()
+        perturb(lat)
+        lat.iterate(3)
+        out.append(lat.fields_interior().cpu().double())
+    fa, fb = out
+    scale = fb.abs().max().item()
+    assert torch.allclose(fa, fb, atol=1e-11 * scale, rtol=1e-11), (fa - fb).abs().max().item()
