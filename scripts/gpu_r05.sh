@@ -71,6 +71,7 @@ heavycounters) export TMPDIR=/tmp
            step "tePSM counters" 600 $O/ctr_tepsm.log python tools/counters.py --tag tepsm_256 --outdir $O/counters --nodes 16777216 --passes 0,1,2,3 -- python3 tools/perf_models.py --models d3q27_tePSM_per_NEBB --n3 256 --steps 5
            step "thermo counters" 600 $O/ctr_thermo.log python tools/counters.py --tag thermo_256 --outdir $O/counters --nodes 16777216 --passes 0,1,2,3 -- python3 tools/perf_models.py --models d3q27_pf_velocity_thermo --n3 256 --steps 5
            step "pf384 fp64 counters" 600 $O/ctr_pf384.log python tools/counters.py --tag pf384_fp64 --outdir $O/counters --nodes 56623104 --passes 0,1,2,3 -- python3 tools/bench_configs.py --configs pf384 --steps 5 --warmup 1 ;;
+tilewaves) step "thermo tile waves A/B" 600 $O/thermo_tw.jsonl python tools/perf_models.py --models d3q27_pf_velocity_thermo --n3 256 --steps 20 --rounds 2 --variants ,tw6,tw8 ;;
 *) echo "unknown step $WHAT"; exit 2 ;;
 esac
 done

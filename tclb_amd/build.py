@@ -59,6 +59,9 @@ VARIANTS = {
     # node-class split stages (DSL add_stage(split=True)) as one kernel; a 2 / 3-waves/SIMD
     # floor on the class-1 kernel of split stages only
     "nosplit": ["-DTCLB_NT_STORE=1", "-DTCLB_NO_SPLIT=1"],
+    # occupancy floors of the LDS tile kernels (k_tile.hpp TCLB_TILE_WAVES)
+    "tw6": ["-DTCLB_NT_STORE=1", "-DTCLB_TILE_WAVES=6"],
+    "tw8": ["-DTCLB_NT_STORE=1", "-DTCLB_TILE_WAVES=8"],
     # class-2 kernels without their 2-wave floor (reproduces the r05m tePSM fault)
     "c2w0": ["-DTCLB_NT_STORE=1", "-DTCLB_SPLIT_WAVES2=0"],
     "cw2": ["-DTCLB_NT_STORE=1", "-DTCLB_SPLIT_WAVES=2"],

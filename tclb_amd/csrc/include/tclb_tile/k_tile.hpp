@@ -24,8 +24,17 @@
 #define TCLB_LDS_TILES 1
 #endif
 
+// occupancy floor of the tile kernels (A/B knob, build variant flag -DTCLB_TILE_WAVES=n)
+#ifndef TCLB_TILE_WAVES
+#define TCLB_TILE_WAVES 0
+#endif
 template <class Model, class R, class S, int STG, bool GLOB>
-__global__ void __launch_bounds__(TILE_BX * TILE_BY) k_tile(const Launch L) {
+#if TCLB_TILE_WAVES > 0
+__global__ void __launch_bounds__(TILE_BX * TILE_BY) __attribute__((amdgpu_waves_per_eu(TCLB_TILE_WAVES)))
+#else
+__global__ void __launch_bounds__(TILE_BX * TILE_BY)
+#endif
+k_tile(const Launch L) {
   typedef typename Model::template NodeTile<R, S, GLOB, STG> N;
   typedef typename N::G_ G;
   constexpr int NT = Model::tile_count(STG);
