@@ -72,6 +72,9 @@ heavycounters) export TMPDIR=/tmp
            step "thermo counters" 600 $O/ctr_thermo.log python tools/counters.py --tag thermo_256 --outdir $O/counters --nodes 16777216 --passes 0,1,2,3 -- python3 tools/perf_models.py --models d3q27_pf_velocity_thermo --n3 256 --steps 5
            step "pf384 fp64 counters" 600 $O/ctr_pf384.log python tools/counters.py --tag pf384_fp64 --outdir $O/counters --nodes 56623104 --passes 0,1,2,3 -- python3 tools/bench_configs.py --configs pf384 --steps 5 --warmup 1 ;;
 tilewaves) step "thermo tile waves A/B" 600 $O/thermo_tw.jsonl python tools/perf_models.py --models d3q27_pf_velocity_thermo --n3 256 --steps 20 --rounds 2 --variants ,tw6,tw8 ;;
+cavitycounters) export TMPDIR=/tmp
+           step "cavity counters" 600 $O/ctr_cavity.log python tools/counters.py --tag cavity_256 --outdir $O/counters --nodes 16777216 --passes 0,1,2,3 -- python3 tools/bench_configs.py --configs cavity --steps 10 --warmup 2
+           step "d3q19 uniform counters" 600 $O/ctr_d3q19.log python tools/counters.py --tag d3q19_256 --outdir $O/counters --nodes 16777216 --passes 0,1,2 -- python3 tools/perf_models.py --models auto_d3q19_BGK --n3 256 --steps 10 ;;
 *) echo "unknown step $WHAT"; exit 2 ;;
 esac
 done
