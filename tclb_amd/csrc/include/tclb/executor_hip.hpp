@@ -284,10 +284,12 @@ struct ClassTiles {
 };
 
 // the tile lists of this launch's geometry, built on first use (one synchronising classify
-// pass); nullptr if that failed (the caller then runs both classes over the full grid).
+// pass), copied out under the lock (the cache may grow or evict behind a caller's back);
+// false if that failed (the caller then runs both classes over the full grid).  An
+// evicted entry's list is released with hipFree, which waits for the device.
 // Node::node_class_(stage): 1, 2, or 0 for a node the stage leaves alone (on no list)
 template <class Model, class R, class S, int STG>
-inline const ClassTiles* class_tiles(const Launch& L, dim3 grid, dim3 block, hipStream_t s) {
+inline bool class_tiles(const Launch& L, dim3 grid, dim3 block, hipStream_t s, ClassTiles& out) {
   static std::vector<ClassTiles> cache;
   static std::mutex mu;
   static unsigned long long clock = 0;
@@ -297,7 +299,8 @@ inline const ClassTiles* class_tiles(const Launch& L, dim3 grid, dim3 block, hip
     if (c.flags == L.flags && c.gen == L.flags_gen && c.bx == block.x && c.by == block.y &&
         std::equal(box, box + 6, c.box)) {
       c.used = ++clock;
-      return &c;
+      out = c;
+      return true;
     }
   }
   // entries of an older identity of these node types are stale; keep at most 32 others
@@ -318,14 +321,14 @@ inline const ClassTiles* class_tiles(const Launch& L, dim3 grid, dim3 block, hip
   }
   const unsigned total = grid.x * grid.y * grid.z;
   unsigned char* d = nullptr;
-  if (hipMalloc(&d, total) != hipSuccess) return nullptr;
+  if (hipMalloc(&d, total) != hipSuccess) return false;
   std::vector<unsigned char> h(total);
   k_classify<Model, R, S, STG><<<grid, block, 0, s>>>(L, d);
   bool ok = hipGetLastError() == hipSuccess &&
             hipMemcpyAsync(h.data(), d, total, hipMemcpyDeviceToHost, s) == hipSuccess &&
             hipStreamSynchronize(s) == hipSuccess;
   hipFree(d);
-  if (!ok) return nullptr;
+  if (!ok) return false;
   std::vector<unsigned> l1, l2;
   for (unsigned b = 0; b < total; b++) {
     if (h[b] & 2) l1.push_back(b);
@@ -344,14 +347,15 @@ inline const ClassTiles* class_tiles(const Launch& L, dim3 grid, dim3 block, hip
   c.list = nullptr;
   l1.insert(l1.end(), l2.begin(), l2.end());
   if (!l1.empty()) {
-    if (hipMalloc(&c.list, l1.size() * sizeof(unsigned)) != hipSuccess) return nullptr;
+    if (hipMalloc(&c.list, l1.size() * sizeof(unsigned)) != hipSuccess) return false;
     if (hipMemcpy(c.list, l1.data(), l1.size() * sizeof(unsigned), hipMemcpyHostToDevice) != hipSuccess) {
       hipFree(c.list);
-      return nullptr;
+      return false;
     }
   }
   cache.push_back(c);
-  return &cache.back();
+  out = c;
+  return true;
 }
 
 template <class Model, class R, class S, int STG, bool GLOB, int CLS>
@@ -458,7 +462,8 @@ inline bool launch_one(const Launch& L, dim3 grid, dim3 block, hipStream_t s) {
   if constexpr (Model::split_stage(I) && !TCLB_NO_SPLIT) {
     // one kernel per node class (the common interior path, then the rest), each over the
     // tiles that hold nodes of its class
-    const ClassTiles* ct = class_tiles<Model, R, S, I>(L, grid, block, s);
+    ClassTiles c;
+    const ClassTiles* ct = class_tiles<Model, R, S, I>(L, grid, block, s, c) ? &c : nullptr;
     launch_class<Model, R, S, I, G, 1>(L, grid, block, s, ct);
     launch_class<Model, R, S, I, G, 2>(L, grid, block, s, ct);
     return true;
