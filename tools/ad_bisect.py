@@ -26,7 +26,8 @@ sys.path.insert(0, ROOT)
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("what", choices=["build", "check", "passes"])
+    ap.add_argument("what", choices=["build", "check", "passes", "ir"])
+    ap.add_argument("--out", default="gpurun_out/ad_ir", help="ir: directory of the IR files")
     ap.add_argument("--limits", default="")
     ap.add_argument("--model", default="d3q19_adj")
     ap.add_argument("--form", default="row_w2")
@@ -37,6 +38,22 @@ def main():
         for n in limits:
             B.build_model(a.model, kinds=("adhip",), variant=f"{a.form}_bis{n}")
             print(json.dumps({"built": f"{a.form}_bis{n}"}), flush=True)
+        return
+    if a.what == "ir":
+        # the device IR of the AD library at each bisection limit (the change between
+        # limits N-1 and N is exactly what pass N did; every later pass is skipped)
+        from tclb_amd.models import registry
+        m = registry.get(a.model)
+        paths = B.emit_model(m)
+        src = B._adhip_source(m, paths["dir"])
+        os.makedirs(a.out, exist_ok=True)
+        for n in limits:
+            out = os.path.join(a.out, f"{a.model}_{a.form}_bis{n}.ll")
+            cmd = B._cmd("adhip", src, out, paths["dir"], f"{a.form}_bis{n}")
+            cmd = cmd[:cmd.index("-o")] + ["--offload-device-only", "-S", "-emit-llvm", "-o", out]
+            r = subprocess.run(cmd, capture_output=True, text=True)
+            print(json.dumps({"limit": n, "ir": out, "rc": r.returncode, "stderr": r.stderr[-300:] if r.returncode else ""}),
+                  flush=True)
         return
     if a.what == "passes":
         # the device passes a limit corresponds to (device-only compile, stderr of the bisection)
