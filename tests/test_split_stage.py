@@ -124,3 +124,24 @@ def test_thermo_nonlocaltemp_adiabatic_nodes():
     fa, fb = out
     scale = fb.abs().max().item()
     assert torch.allclose(fa, fb, atol=1e-11 * scale, rtol=1e-11), (fa - fb).abs().max().item()
+
+
+@pytest.mark.gpu
+@needs_gpu
+def test_thermo_parabolic_surface_tension():
+    """surfPower > 1 takes the out-of-line power law (d3q27_pf_velocity.inc pow_cold_, a
+    real call in the GPU kernels): GPU equals CPU"""
+    name = "d3q27_pf_velocity_thermo"
+    out = []
+    for dev in ("cuda", "cpu"):
+        lat = make_case(name, dev, shape=(32, 16, 12))
+        lat.set_setting("surfPower", 2.0)
+        lat.set_setting("sigma_TT", 1e-4)
+        lat.set_setting("T_ref", 0.5)
+        lat.init()
+        perturb(lat)
+        lat.iterate(3)
+        out.append(lat.fields_interior().cpu().double())
+    fa, fb = out
+    scale = fb.abs().max().item()
+    assert torch.allclose(fa, fb, atol=1e-11 * scale, rtol=1e-11), (fa - fb).abs().max().item()
