@@ -75,6 +75,8 @@ tilewaves) step "thermo tile waves A/B" 600 $O/thermo_tw.jsonl python tools/perf
 cavitycounters) export TMPDIR=/tmp
            step "cavity counters" 600 $O/ctr_cavity.log python tools/counters.py --tag cavity_256 --outdir $O/counters --nodes 16777216 --passes 0,1,2,3 -- python3 tools/bench_configs.py --configs cavity --steps 10 --warmup 2
            step "d3q19 uniform counters" 600 $O/ctr_d3q19.log python tools/counters.py --tag d3q19_256 --outdir $O/counters --nodes 16777216 --passes 0,1,2 -- python3 tools/perf_models.py --models auto_d3q19_BGK --n3 256 --steps 10 ;;
+cwab) step "pf384 fp64 class-1 floor A/B" 600 $O/pf384_cw_fp64.jsonl python tools/perf_models.py --models d3q27_pf_velocity --n3 384 --steps 20 --rounds 2 --variants ,cw3
+      step "pf384 mixed-shift class-1 floor A/B" 600 $O/pf384_cw_ms.jsonl python tools/perf_models.py --models d3q27_pf_velocity --n3 384 --steps 20 --rounds 2 --variants ,cw3,cw4 --precision mixed-shift ;;
 *) echo "unknown step $WHAT"; exit 2 ;;
 esac
 done

@@ -66,6 +66,7 @@ VARIANTS = {
     "c2w0": ["-DTCLB_NT_STORE=1", "-DTCLB_SPLIT_WAVES2=0"],
     "cw2": ["-DTCLB_NT_STORE=1", "-DTCLB_SPLIT_WAVES=2"],
     "cw3": ["-DTCLB_NT_STORE=1", "-DTCLB_SPLIT_WAVES=3"],
+    "cw4": ["-DTCLB_NT_STORE=1", "-DTCLB_SPLIT_WAVES=4"],
     # the round-2 form everywhere: flat accessors, register globals, no uniform-y hint
     # scheduler A/B: memory clauses grouped by the AMDGPU machine scheduler
     "mclause": ["-DTCLB_NT_STORE=1", "-mllvm", "-amdgpu-sched-strategy=max-memory-clause"],
