@@ -351,9 +351,12 @@ def stale_reason(name: str, kind: str, variant: str = "") -> Optional[str]:
 
 
 def build_model(name: str, kinds=("cpu", "hip"), force: bool = False, verbose: bool = False,
-                variant: str = "") -> Dict[str, str]:
+                variant: str = "", paths: Optional[Dict[str, str]] = None) -> Dict[str, str]:
+    """compile one model's libraries of the given kinds (skipped when the stamped inputs
+    are unchanged); paths: the model's emit_model result, when the caller emitted it
+    already (build_all emits every model once, then compiles its kinds in parallel)"""
     model = registry.get(name)
-    paths = emit_model(model)
+    paths = paths or emit_model(model)
     os.makedirs(LIB, exist_ok=True)
     out = {}
     for kind in kinds:
@@ -576,14 +579,13 @@ def build_all(models: Optional[List[str]] = None, kinds=("cpu", "hip"), jobs: in
     tasks = [(m, k) for m in models for k in kinds]
     res: Dict[str, Dict[str, str]] = {m: {} for m in models}
     # emit serially (sympy + file writes), compile in parallel
-    for m in models:
-        emit_model(registry.get(m))
+    emitted = {m: emit_model(registry.get(m)) for m in models}
     errors = []
 
     def one(t):
         m, k = t
         try:
-            return m, k, build_model(m, kinds=(k,), force=force, verbose=verbose).get(k), None
+            return m, k, build_model(m, kinds=(k,), force=force, verbose=verbose, paths=emitted[m]).get(k), None
         except Exception as e:  # noqa
             return m, k, None, e
 
@@ -607,12 +609,11 @@ def build_adjoint_libs(models: Optional[List[str]] = None, jobs: int = 0, force=
     models = models or sorted(ADJOINT_MODELS | {"d2q9_kuper"})
     kinds = ("ad", "adhip") if os.path.exists(HIPCC) else ("ad",)
     jobs = jobs or max(1, min(8, os.cpu_count() or 1))
-    for m in models:
-        emit_model(registry.get(m))
+    emitted = {m: emit_model(registry.get(m)) for m in models}
 
     def one(t):
         m, k = t
-        return m, k, build_model(m, kinds=(k,), force=force, verbose=verbose).get(k)
+        return m, k, build_model(m, kinds=(k,), force=force, verbose=verbose, paths=emitted[m]).get(k)
 
     res: Dict[str, Dict[str, str]] = {m: {} for m in models}
     with ThreadPoolExecutor(max_workers=jobs) as ex:
