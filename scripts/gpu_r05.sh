@@ -77,6 +77,7 @@ cavitycounters) export TMPDIR=/tmp
            step "d3q19 uniform counters" 600 $O/ctr_d3q19.log python tools/counters.py --tag d3q19_256 --outdir $O/counters --nodes 16777216 --passes 0,1,2 -- python3 tools/perf_models.py --models auto_d3q19_BGK --n3 256 --steps 10 ;;
 cwab) step "pf384 fp64 class-1 floor A/B" 600 $O/pf384_cw_fp64.jsonl python tools/perf_models.py --models d3q27_pf_velocity --n3 384 --steps 20 --rounds 2 --variants ,cw3
       step "pf384 mixed-shift class-1 floor A/B" 600 $O/pf384_cw_ms.jsonl python tools/perf_models.py --models d3q27_pf_velocity --n3 384 --steps 20 --rounds 2 --variants ,cw3,cw4 --precision mixed-shift ;;
+catalog) step "catalog perf (all models, guard on)" 1150 $O/catalog_perf.jsonl python tools/perf_models.py --n3 192 --n2 2048 --steps 10 --allow-invalid ;;
 *) echo "unknown step $WHAT"; exit 2 ;;
 esac
 done
