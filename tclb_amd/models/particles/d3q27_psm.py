@@ -84,7 +84,8 @@ def build(ms=False, kl=False, trt=False, nebb=False, sup=False, singlekernel=Fal
     elif particles:
         m.add_stage("BaseInit", "Init", save_fields=save)
         m.add_stage("BaseIteration", "Run", save_fields=save, load_densities=load + ["Force"])
-        m.add_stage("CalcF", "CalcF", save_fields=["Force"], load_densities=load, particle=True)
+        # lazy: the populations are pulled only within reach of a particle (d3q27_psm.inc CalcF)
+        m.add_stage("CalcF", "CalcF", save_fields=["Force"], load_densities=load, particle=True, lazy_load=True)
         m.add_action("Iteration", ["BaseIteration", "CalcF"])
         m.add_action("Init", ["BaseInit", "CalcF"])
     else:
