@@ -80,6 +80,8 @@ cwab) step "pf384 fp64 class-1 floor A/B" 600 $O/pf384_cw_fp64.jsonl python tool
 catalog) step "catalog perf (all models, guard on)" 1150 $O/catalog_perf.jsonl python tools/perf_models.py --n3 192 --n2 2048 --steps 10 --allow-invalid ;;
 psm) step "PSM GPU tests" 600 $O/pytest_psm.log python -u -m pytest tests -v -m gpu -k "PSM or psm or particle" --timeout 120 --timeout-method thread -p no:cacheprovider
      step "PSM perf" 600 $O/psm_perf.jsonl python tools/perf_models.py --models d3q27_PSM_NEBB,d3q27_PSM_SUP,d3q27_PSM_MS_NEBB,d3q27_PSM_KL_NEBB,d3q27_PSM_TRT_NEBB,d3q27_PSM_NEBB_singlekernel --n3 192 --steps 10 --rounds 2 ;;
+cumpart) step "cumulant/particle GPU tests" 600 $O/pytest_cumpart.log python -u -m pytest tests -v -m gpu -k "cumulant or particle or part" --timeout 120 --timeout-method thread -p no:cacheprovider
+         step "cumulant_part perf" 600 $O/cumpart_perf.jsonl python tools/perf_models.py --models d3q27_cumulant_part,d3q27_cumulant_part_AVG_IB_SMAG,d3q27_cumulant --n3 192 --steps 10 --rounds 2 ;;
 *) echo "unknown step $WHAT"; exit 2 ;;
 esac
 done

@@ -43,7 +43,9 @@ def build(avg: bool = False, ib: bool = False, smag: bool = False, part: bool = 
                       comment="(local) particle velocity limit")
         m.add_stage("BaseIteration", "Run", save_fields=["f", "Force", "avg"], load_densities=["f", "Force", "avg"])
         m.add_stage("BaseInit", "Init", save_fields=["f", "Force", "avg"])
-        m.add_stage("CalcF", "CalcF", save_fields=["Force"], load_densities=["f", "Force"], particle=True)
+        # lazy: the populations are pulled only within reach of a particle
+        m.add_stage("CalcF", "CalcF", save_fields=["Force"], load_densities=["f", "Force"], particle=True,
+                    lazy_load=True)
         m.add_action("Iteration", ["BaseIteration", "CalcF"])
         m.add_action("Init", ["BaseInit", "CalcF"])
     m.add_setting("nu", default=0.16666666, comment="Viscosity")
