@@ -124,7 +124,7 @@ def main():
                     help="globals on every step (a <Log Iterations=\"1\">-style run), not only the last")
     ap.add_argument("--loopback-dist", action="store_true",
                     help="1 rank through the multi-rank path (border/interior split + pack/unpack)")
-    ap.add_argument("--transport", default=None, choices=["rccl", "copy"],
+    ap.add_argument("--transport", default=None, choices=["rccl", "copy", "ipc"],
                     help="halo transport of --loopback-dist (rccl: RCCL send/receive to itself)")
     ap.add_argument("--python-loop", action="store_true",
                     help="multi-rank steps from the Python step path instead of the native loop (A/B)")

@@ -1,0 +1,30 @@
+#!/bin/bash
+# halo-exchange A/B on one MI355X (round 6): the per-rank slab shapes of the 8-GPU
+# headline (512x512x64 fp64) and the 4-GPU part256 case (256x256x64) stepped as one rank
+# through the multi-rank loop with each transport (copy / RCCL to itself / IPC pull from
+# itself), against the plain one-rank lattice; kernel traces of the RCCL and IPC steps.
+#   TAG=r06a scripts/halo_ab.sh [tests] [ab] [prof]
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}; TAG=${TAG:-halo}; O=$R/gpurun_out/$TAG; mkdir -p $O; cd $R
+step() { local name=$1 t=$2 log=$3; shift 3; echo "== $name"; timeout -k 10 $t "$@" > $log 2>&1; local rc=$?; tail -3 $log; echo "   rc=$rc"; if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi; return 0; }
+export TMPDIR=/tmp
+for W in "$@"; do case $W in
+tests)
+  step "ipc + production tests" 600 $O/pytest_ipc.log python -u -m pytest tests/test_gpu_ipc.py tests/test_gpu_production.py -v -m gpu --timeout 300 --timeout-method thread ;;
+ab)
+  for rep in $(seq 1 ${REPS:-2}); do
+    step "slab plain" 300 $O/slab_plain_$rep.json python bench.py --shape 512,512,64 --steps 200 --warmup 20
+    for t in copy rccl ipc; do
+      step "slab $t" 300 $O/slab_${t}_$rep.json python bench.py --shape 512,512,64 --steps 200 --warmup 20 --loopback-dist --transport $t
+    done
+    step "part slab plain" 300 $O/part_plain_$rep.jsonl python tools/bench_configs.py --configs part256 --shape 256,256,64 --steps 200 --warmup 20
+    for t in copy rccl ipc; do
+      step "part slab $t" 300 $O/part_${t}_$rep.jsonl python tools/bench_configs.py --configs part256 --shape 256,256,64 --steps 200 --warmup 20 --loopback-dist --transport $t
+    done
+  done ;;
+prof)
+  for t in rccl ipc; do
+    step "rocprof slab $t" 400 $O/prof_slab_$t.log rocprofv3 --kernel-trace --stats -d $O/prof_slab_$t -o run --output-format csv -- python3 $R/bench.py --shape 512,512,64 --steps 20 --warmup 2 --loopback-dist --transport $t
+    step "rocprof part slab $t" 400 $O/prof_part_$t.log rocprofv3 --kernel-trace --stats -d $O/prof_part_$t -o run --output-format csv -- python3 $R/tools/bench_configs.py --configs part256 --shape 256,256,64 --steps 20 --warmup 2 --loopback-dist --transport $t
+  done ;;
+esac; done

@@ -16,9 +16,11 @@
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <chrono>
+#include <thread>
 
 #include "tclb_rt/ad_loop.hpp"
 #include "tclb_rt/dist_loop.hpp"
@@ -87,13 +89,28 @@ int load_rccl(const char* path, Rccl& R) {
   return 0;
 }
 
+// IPC transport signal block: one monotonically increasing counter per word, each on its
+// own 128-byte line; A = the slab / grid-z phase, B = the grid's y phase, R = the particle
+// force all-reduce; READY: this rank's send data of exchange e is in place, DONE: this rank
+// has pulled its neighbours' data of exchange e; ERR: a wait of this rank timed out
+enum { SIG_A_READY = 0, SIG_A_DONE, SIG_B_READY, SIG_B_DONE, SIG_R_READY, SIG_R_DONE, SIG_ERR, SIG_WORDS };
+constexpr int SIG_STRIDE = 16;   // words between counters
+constexpr size_t SIG_BYTES = sizeof(unsigned long long) * SIG_STRIDE * SIG_WORDS;
+constexpr int IPC_MAX_RANKS = 64;   // one wave polls every rank's counter
+
 struct Ctx {
-  int transport;  // 0 = device copies (loopback), 1 = RCCL
+  int transport;  // 0 = device copies (loopback), 1 = RCCL, 3 = IPC (peer memory pulls)
   int nranks, rank;
   Rccl R;
   Comm comm = nullptr;
   hipStream_t cs = nullptr;   // comm stream
   hipEvent_t ready = nullptr, done = nullptr;
+  // IPC transport
+  unsigned long long* sig = nullptr;              // this rank's signal block (exported)
+  unsigned long long* hsig[IPC_MAX_RANKS] = {};   // every rank's, mapped (host table)
+  unsigned long long** dsig = nullptr;            // the same table on the device
+  unsigned long long seq[3] = {0, 0, 0};          // exchange counters of A, B, R
+  long long ticks = 0;                            // wait timeout in wall-clock ticks
 };
 
 int rccl_check(Ctx* c, int r, const char* what) {
@@ -126,6 +143,31 @@ __global__ void __launch_bounds__(256) k_pack(T* snap, T* stg, long long fs, lon
   else stg[i] = *a;
 }
 
+// the contiguous segments of a packed phase A (tclb_rt/dist_loop.hpp SegOp), one launch
+// for all of them: blockIdx.y picks the segment, the x blocks stride over its V words
+struct Peers {
+  const char* p[4];
+};
+
+template <class V>
+__global__ void __launch_bounds__(256) k_segcopy(const tclb::SegOp* segs, char* snap, char* stg, Peers peers) {
+  const tclb::SegOp o = segs[blockIdx.y];
+  char* d;
+  const char* s;
+  if (o.dir == 0) {
+    d = stg + o.dst, s = snap + o.src;
+  } else if (o.dir == 1) {
+    d = snap + o.dst, s = stg + o.src;
+  } else {
+    const char* b = o.peer == 0 ? peers.p[0] : o.peer == 1 ? peers.p[1] : o.peer == 2 ? peers.p[2] : peers.p[3];
+    d = (o.dir == 2 ? snap : stg) + o.dst, s = b + o.src;
+  }
+  const long long nv = o.bytes / (long long)sizeof(V);
+  const long long step = (long long)gridDim.x * blockDim.x;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += step)
+    ((V*)d)[i] = ((const V*)s)[i];
+}
+
 // active entries of the zonal time series: zonal[idx] = v[iter % len] (and the slope)
 __global__ void k_series(double* zonal, const tclb::SeriesEntry* E, int n, const double* v, const double* dv,
                          int iter) {
@@ -135,6 +177,44 @@ __global__ void k_series(double* zonal, const tclb::SeriesEntry* E, int n, const
   const int k = iter % e.len;
   zonal[e.idx] = v[e.off + k];
   if (e.len > 1) zonal[e.dtidx] = dv[e.off + k];
+}
+
+// IPC transport: publish counter value v (after everything earlier on the stream)
+__global__ void k_signal(unsigned long long* f, unsigned long long v) {
+  if (threadIdx.x == 0) {
+    __threadfence_system();
+    __hip_atomic_store(f, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+// IPC transport: lane r waits until rank r's counter `word` reaches v, for every rank in
+// `mask`.  Bounded: after `ticks` of the constant wall clock the lane flags *err and
+// leaves (a dead peer ends in an error the host reads, never in a wave that spins
+// forever); once *err is set every later wait returns at once.
+__global__ void k_wait(unsigned long long* const* tab, unsigned long long mask, int word, unsigned long long v,
+                       unsigned long long* err, long long ticks) {
+  const int r = threadIdx.x;
+  if (r >= 64 || !((mask >> r) & 1ull)) return;
+  if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0) return;
+  const unsigned long long* f = tab[r] + word;
+  const long long t0 = wall_clock64();
+  while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < v) {
+    if (wall_clock64() - t0 > ticks) {
+      __hip_atomic_store(err, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      return;
+    }
+    __builtin_amdgcn_s_sleep(4);
+  }
+}
+
+// IPC transport: the particle force all-reduce, every rank summing the ranks' shared
+// copies in rank order (the same sum, bit for bit, on every rank)
+__global__ void __launch_bounds__(256) k_accsum(double* out, const double* const* accs, int nranks, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  double s = accs[0][i];
+  for (int r = 1; r < nranks; r++) s += accs[r][i];
+  out[i] = s;
 }
 
 __global__ void __launch_bounds__(256) k_nan0(double* a, int n) {
@@ -225,12 +305,92 @@ struct GpuSvc {
     return 0;
   }
 
-  int xstart(char* base, const tclb::LoopPlan& P, const tclb::StagePlan& st) {
+  // one launch over segments [s0, s0 + n) of the plan, on the comm stream
+  int segcopy(char* base, char* stg, const tclb::LoopPlan& P, int s0, int n) {
+    if (n <= 0) return 0;
+    long long align = 0, maxb = 0;
+    for (int i = 0; i < n; i++) {
+      const tclb::SegOp& o = P.segs[s0 + i];
+      align |= o.dst | o.src | o.bytes;
+      if (o.bytes > maxb) maxb = o.bytes;
+    }
+    const int w = (align & 15) == 0 ? 16 : (align & 7) == 0 ? 8 : (align & 3) == 0 ? 4 : (align & 1) == 0 ? 2 : 1;
+    long long bx = (maxb / w + 255) / 256;
+    if (bx > 1024) bx = 1024;
+    if (bx < 1) bx = 1;
+    const dim3 grid((unsigned)bx, (unsigned)n);
+    const tclb::SegOp* d = P.dsegs + s0;
+    Peers pe;
+    for (int i = 0; i < 4; i++) pe.p[i] = (const char*)P.peer_stg[i];
+    switch (w) {
+      case 16: k_segcopy<uint4><<<grid, 256, 0, c->cs>>>(d, base, stg, pe); break;
+      case 8: k_segcopy<uint2><<<grid, 256, 0, c->cs>>>(d, base, stg, pe); break;
+      case 4: k_segcopy<unsigned><<<grid, 256, 0, c->cs>>>(d, base, stg, pe); break;
+      case 2: k_segcopy<unsigned short><<<grid, 256, 0, c->cs>>>(d, base, stg, pe); break;
+      default: k_segcopy<unsigned char><<<grid, 256, 0, c->cs>>>(d, base, stg, pe); break;
+    }
+    return hip_check(hipGetLastError(), "k_segcopy");
+  }
+
+  // IPC transport primitives (see k_signal / k_wait)
+  int signal(hipStream_t s, int word, unsigned long long v) {
+    k_signal<<<1, 64, 0, s>>>(c->sig + word * SIG_STRIDE, v);
+    return hip_check(hipGetLastError(), "k_signal");
+  }
+  int wait(hipStream_t s, unsigned long long mask, int word, unsigned long long v) {
+    if (!mask) return 0;
+    k_wait<<<1, 64, 0, s>>>(c->dsig, mask, word * SIG_STRIDE, v, c->sig + SIG_ERR * SIG_STRIDE, c->ticks);
+    return hip_check(hipGetLastError(), "k_wait");
+  }
+  static unsigned long long peer_mask(const tclb::LoopPlan& P, int a, int b) {
+    unsigned long long m = 0;
+    if (P.ipc_peer[a] >= 0) m |= 1ull << P.ipc_peer[a];
+    if (P.ipc_peer[b] >= 0) m |= 1ull << P.ipc_peer[b];
+    return m;
+  }
+
+  // the exchange of one stage over IPC-mapped peer memory, on the comm stream: publish
+  // READY, wait for the neighbours' READY, pull their packed send buffers straight into
+  // the ghost planes (one copy launch), publish DONE; the grid's y phase the same way
+  // through the staging rows; finally wait for the neighbours' DONE, so nothing of this
+  // rank's send buffers is rewritten (next stage / step) before they have been read.
+  // Reference: MPIStream_A / MPIStream_B (src/Lattice.cu.Rt:327-389), here without MPI
+  // or a collective library — a one-sided pull between the processes of one node.
+  int xstart_ipc(char* base, const tclb::LoopPlan& P, const tclb::StagePlan& st, int mirrored) {
     int r;
     char* stg = (char*)P.staging;
     if ((r = hip_check(hipEventRecord(c->ready, ks), "hipEventRecord")) != 0) return r;
     if ((r = hip_check(hipStreamWaitEvent(c->cs, c->ready, 0), "hipStreamWaitEvent")) != 0) return r;
+    const unsigned long long mA = peer_mask(P, 0, 1), mB = peer_mask(P, 2, 3);
+    const unsigned long long e = ++c->seq[0];
+    if (!mirrored && (r = segcopy(base, stg, P, st.seg0, st.npack)) != 0) return r;
+    if ((r = signal(c->cs, SIG_A_READY, e)) != 0 || (r = wait(c->cs, mA, SIG_A_READY, e)) != 0) return r;
+    if ((r = segcopy(base, stg, P, st.seg0 + st.npack, st.nunpack)) != 0) return r;
+    if ((r = signal(c->cs, SIG_A_DONE, e)) != 0) return r;
+    if (st.npk > 0 || st.nyseg > 0) {
+      const unsigned long long eb = ++c->seq[1];
+      if ((r = packs(base, stg, P.packs + st.pk0, st.npk, 0)) != 0) return r;
+      if ((r = signal(c->cs, SIG_B_READY, eb)) != 0 || (r = wait(c->cs, mB, SIG_B_READY, eb)) != 0) return r;
+      if ((r = segcopy(base, stg, P, st.yseg0, st.nyseg)) != 0) return r;
+      if ((r = packs(base, stg, P.packs + st.pk0, st.npk, 1)) != 0) return r;
+      if ((r = signal(c->cs, SIG_B_DONE, eb)) != 0 || (r = wait(c->cs, mB, SIG_B_DONE, eb)) != 0) return r;
+    }
+    if ((r = wait(c->cs, mA, SIG_A_DONE, e)) != 0) return r;
+    return hip_check(hipEventRecord(c->done, c->cs), "hipEventRecord");
+  }
+
+  // the exchange of one stage on the comm stream, ordered after the work on ks: phase A
+  // (pack unless the border launches mirrored their stores, one send and one receive per
+  // neighbour, unpack), then the grid's y phase (row packs, sends / receives, unpacks)
+  int xstart(char* base, const tclb::LoopPlan& P, const tclb::StagePlan& st, int mirrored) {
+    if (c->transport == 3) return xstart_ipc(base, P, st, mirrored);
+    int r;
+    char* stg = (char*)P.staging;
+    if ((r = hip_check(hipEventRecord(c->ready, ks), "hipEventRecord")) != 0) return r;
+    if ((r = hip_check(hipStreamWaitEvent(c->cs, c->ready, 0), "hipStreamWaitEvent")) != 0) return r;
+    if (!mirrored && (r = segcopy(base, stg, P, st.seg0, st.npack)) != 0) return r;
     if ((r = p2p(base, stg, P.ops + st.op0, st.nops)) != 0) return r;
+    if ((r = segcopy(base, stg, P, st.seg0 + st.npack, st.nunpack)) != 0) return r;
     if (st.nopsb > 0) {
       if ((r = packs(base, stg, P.packs + st.pk0, st.npk, 0)) != 0) return r;
       if ((r = p2p(base, stg, P.ops + st.opb0, st.nopsb)) != 0) return r;
@@ -273,6 +433,19 @@ struct GpuSvc {
       if ((r = rccl_check(c, c->R.all_reduce(q.acc, q.acc, (size_t)na, 8, 0, c->comm, ks), "ncclAllReduce")) != 0)
         return r;
     }
+    if (q.allreduce && c->transport == 3 && c->nranks > 1 && na > 0) {
+      // publish a copy, wait for every rank's, sum them in rank order, and wait until
+      // every rank has summed before the copy may be rewritten
+      const unsigned long long e = ++c->seq[2];
+      const unsigned long long all = c->nranks >= 64 ? ~0ull : ((1ull << c->nranks) - 1);
+      if ((r = hip_check(hipMemcpyAsync(q.accbuf, q.acc, sizeof(double) * (size_t)na, hipMemcpyDeviceToDevice, ks),
+                         "hipMemcpyAsync")) != 0)
+        return r;
+      if ((r = signal(ks, SIG_R_READY, e)) != 0 || (r = wait(ks, all, SIG_R_READY, e)) != 0) return r;
+      k_accsum<<<(na + 255) / 256, 256, 0, ks>>>(q.acc, q.accs, c->nranks, na);
+      if ((r = hip_check(hipGetLastError(), "k_accsum")) != 0) return r;
+      if ((r = signal(ks, SIG_R_DONE, e)) != 0 || (r = wait(ks, all, SIG_R_DONE, e)) != 0) return r;
+    }
     if (na > 0) {
       k_nan0<<<(na + 255) / 256, 256, 0, ks>>>(q.acc, na);
       if ((r = hip_check(hipGetLastError(), "k_nan0")) != 0) return r;
@@ -310,6 +483,8 @@ int tclb_dist_unique_id(const char* rccl_path, void* out) {
 }
 
 // transport 0: device copies (nranks must be 1); 1: RCCL communicator of nranks ranks
+void tclb_dist_ctx_destroy(void* ctx);
+
 void* tclb_dist_ctx_create(const char* rccl_path, int transport, int nranks, int rank, const void* uid) {
   Ctx* c = new Ctx();
   c->transport = transport;
@@ -336,6 +511,31 @@ void* tclb_dist_ctx_create(const char* rccl_path, int transport, int nranks, int
       delete c;
       return nullptr;
     }
+  } else if (transport == 3) {
+    if (nranks > IPC_MAX_RANKS) {
+      set_err("tclb_dist_ctx_create", "the IPC transport takes at most 64 ranks");
+      delete c;
+      return nullptr;
+    }
+    // the signal block: uncached device memory, so a wave polling a counter of another
+    // process (same device or a peer over xGMI) reads memory, never a stale cache line
+    if (hipExtMallocWithFlags((void**)&c->sig, SIG_BYTES, hipDeviceMallocUncached) != hipSuccess &&
+        hip_check(hipMalloc((void**)&c->sig, SIG_BYTES), "hipMalloc") != 0) {
+      delete c;
+      return nullptr;
+    }
+    int khz = 0, dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hip_check(hipMemset(c->sig, 0, SIG_BYTES), "hipMemset") != 0 ||
+        hip_check(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev), "hipDeviceGetAttribute") != 0 ||
+        hip_check(hipMalloc((void**)&c->dsig, sizeof(void*) * IPC_MAX_RANKS), "hipMalloc") != 0) {
+      tclb_dist_ctx_destroy(c);
+      return nullptr;
+    }
+    const char* t = getenv("TCLB_IPC_TIMEOUT_S");
+    const double sec = t ? atof(t) : 120.0;
+    c->ticks = (long long)((double)(khz > 0 ? khz : 100000) * 1000.0 * sec);
+    c->hsig[rank] = c->sig;
   } else if (nranks != 1) {
     set_err("tclb_dist_ctx_create", "the copy transport is single-rank");
     delete c;
@@ -344,11 +544,75 @@ void* tclb_dist_ctx_create(const char* rccl_path, int transport, int nranks, int
   return c;
 }
 
+// ---- IPC transport: shared buffers, the signal blocks, the error flag
+
+// device memory another process can map: zeroed, its handle (64 bytes) into handle_out
+void* tclb_ipc_alloc(long long bytes, void* handle_out) {
+  void* p = nullptr;
+  if (hip_check(hipMalloc(&p, (size_t)(bytes > 0 ? bytes : 1)), "hipMalloc") != 0) return nullptr;
+  hipIpcMemHandle_t h;
+  if (hip_check(hipMemset(p, 0, (size_t)(bytes > 0 ? bytes : 1)), "hipMemset") != 0 ||
+      hip_check(hipIpcGetMemHandle(&h, p), "hipIpcGetMemHandle") != 0) {
+    (void)hipFree(p);
+    return nullptr;
+  }
+  memcpy(handle_out, &h, sizeof h);
+  return p;
+}
+void tclb_ipc_free(void* p) {
+  if (p) (void)hipFree(p);
+}
+void* tclb_ipc_open(const void* handle) {
+  hipIpcMemHandle_t h;
+  memcpy(&h, handle, sizeof h);
+  void* p = nullptr;
+  if (hip_check(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess), "hipIpcOpenMemHandle") != 0) return nullptr;
+  return p;
+}
+void tclb_ipc_close(void* p) {
+  if (p) (void)hipIpcCloseMemHandle(p);
+}
+int tclb_ipc_handle_bytes() { return (int)sizeof(hipIpcMemHandle_t); }
+
+int tclb_dist_sig_handle(void* ctx, void* out) {
+  Ctx* c = (Ctx*)ctx;
+  hipIpcMemHandle_t h;
+  const int r = hip_check(hipIpcGetMemHandle(&h, c->sig), "hipIpcGetMemHandle(signals)");
+  if (r == 0) memcpy(out, &h, sizeof h);
+  return r;
+}
+
+// map every other rank's signal block (handles: nranks x 64 bytes, rank order)
+int tclb_dist_sig_attach(void* ctx, const char* handles) {
+  Ctx* c = (Ctx*)ctx;
+  for (int k = 0; k < c->nranks; k++) {
+    if (k == c->rank) continue;
+    void* p = tclb_ipc_open(handles + (size_t)k * sizeof(hipIpcMemHandle_t));
+    if (!p) return -20;
+    c->hsig[k] = (unsigned long long*)p;
+  }
+  return hip_check(hipMemcpy(c->dsig, c->hsig, sizeof(void*) * IPC_MAX_RANKS, hipMemcpyHostToDevice), "hipMemcpy");
+}
+
+// 1: a wait of this rank timed out (a peer stopped publishing); reads the flag
+// synchronously (call when the rank's queued work has been waited for)
+int tclb_dist_ipc_error(void* ctx) {
+  Ctx* c = (Ctx*)ctx;
+  if (!c || c->transport != 3 || !c->sig) return 0;
+  unsigned long long v = 0;
+  if (hipMemcpy(&v, c->sig + SIG_ERR * SIG_STRIDE, sizeof v, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+  return v ? 1 : 0;
+}
+
 void tclb_dist_ctx_destroy(void* ctx) {
   Ctx* c = (Ctx*)ctx;
   if (!c) return;
   if (c->cs) (void)hipStreamSynchronize(c->cs);
   if (c->comm) c->R.comm_destroy(c->comm);
+  for (int k = 0; k < IPC_MAX_RANKS; k++)
+    if (c->hsig[k] && k != c->rank) (void)hipIpcCloseMemHandle(c->hsig[k]);
+  if (c->sig) (void)hipFree(c->sig);
+  if (c->dsig) (void)hipFree(c->dsig);
   if (c->ready) (void)hipEventDestroy(c->ready);
   if (c->done) (void)hipEventDestroy(c->done);
   if (c->cs) (void)hipStreamDestroy(c->cs);
@@ -362,7 +626,15 @@ int tclb_loop_iterate(void* ctx, const tclb::Launch* L, int prec, int es, int ns
                       const tclb::LoopPlan* P, tclb::run_fn run, tclb::sample_fn sample) {
   Ctx* c = (Ctx*)ctx;
   GpuSvc sv{c, (hipStream_t)L->stream, prec, run, sample, es, L->fs, L->sz, L->sy, L->px};
-  return tclb::action_loop(sv, *L, nsteps, glob_last, *P, init);
+  const int r = tclb::action_loop(sv, *L, nsteps, glob_last, *P, init);
+  if (r != 0) return r;
+  // a communicator that failed while these steps were queued (a dead peer) is reported
+  // here, not only by tclb_dist_wait, so loops without a globals wait still raise
+  if (c->transport == 1 && c->comm) {
+    int ae = 0;
+    if (c->R.async_error(c->comm, &ae) == 0 && ae != 0) return rccl_check(c, ae, "RCCL async error");
+  }
+  return 0;
 }
 
 // one exchange outside the loop (the Python step path of the same plan)
@@ -373,7 +645,17 @@ int tclb_dist_exchange(void* ctx, void* base, const tclb::HaloOp* ops, int nops,
   tclb::StagePlan st = {};
   P.ops = ops;
   st.nops = nops;
-  int r = sv.xstart((char*)base, P, st);
+  int r = sv.xstart((char*)base, P, st, 1);
+  return r != 0 ? r : sv.xfinish();
+}
+
+// the exchange of stage k of a plan outside the loop (Lattice.exchange on a rank whose
+// halos travel through the loop's transport: after set_fields_interior, a restart, ...)
+int tclb_loop_exchange(void* ctx, void* base, const tclb::LoopPlan* P, int k, int es, long long fs, long long sz,
+                       long long sy, int px, void* stream) {
+  Ctx* c = (Ctx*)ctx;
+  GpuSvc sv{c, (hipStream_t)stream, 0, nullptr, nullptr, es, fs, sz, sy, px};
+  const int r = sv.xstart((char*)base, *P, P->st[k], 0);
   return r != 0 ? r : sv.xfinish();
 }
 
@@ -407,6 +689,7 @@ int tclb_dist_wait(void* ctx, void* stream, int timeout_ms) {
         break;
       }
     }
+    std::this_thread::sleep_for(std::chrono::microseconds(20));
     if (timeout_ms > 0 && (++spins & 1023) == 0 &&
         std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count() > timeout_ms) {
       set_err("tclb_dist_wait", "timed out: aborting the communicator");
@@ -419,6 +702,10 @@ int tclb_dist_wait(void* ctx, void* stream, int timeout_ms) {
     }
   }
   (void)hipEventDestroy(e);
+  if (r == 0 && c->transport == 3 && tclb_dist_ipc_error(c) != 0) {
+    set_err("IPC transport", "a wait for a peer's counter timed out (TCLB_IPC_TIMEOUT_S)");
+    r = -111;
+  }
   return r;
 }
 
@@ -437,5 +724,7 @@ int tclb_loop_sizeof_part() { return (int)sizeof(tclb::PartPlan); }
 int tclb_loop_sizeof_pack() { return (int)sizeof(tclb::PackOp); }
 int tclb_loop_sizeof_series() { return (int)sizeof(tclb::SeriesEntry); }
 int tclb_dist_sizeof_op() { return (int)sizeof(tclb::HaloOp); }
+int tclb_loop_sizeof_seg() { return (int)sizeof(tclb::SegOp); }
+int tclb_loop_sizeof_mirror() { return (int)sizeof(tclb::MirrorSpec); }
 
 }  // extern "C"

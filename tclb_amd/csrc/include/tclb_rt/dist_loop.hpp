@@ -72,6 +72,27 @@ struct PackOp {
   int reserved;
 };
 
+// one contiguous copy of the packed phase A (a field's g halo planes are contiguous in
+// the [field][z][y][x] layout): dir 0 packs snapshot + src -> staging + dst (before the
+// sends, when the border launches did not mirror their stores), dir 1 unpacks staging +
+// src -> snapshot + dst (after the receives); IPC transport: dir 2 pulls a neighbour's
+// packed send buffer (LoopPlan.peer_stg[peer] + src, mapped from the other process) into
+// snapshot + dst, dir 3 into staging + dst (the grid's y rows, unpacked by PackOps)
+struct SegOp {
+  long long dst, src, bytes;
+  int dir;
+  int peer;
+};
+
+// the halo mirror of one border launch (core.hpp mirror_store): the stores of the fields
+// with slot[f] >= 0 also land in staging + boff, packed [slot][g planes]
+struct MirrorSpec {
+  long long boff;
+  long long mfs, msy, msz;
+  int moy, moz;
+  signed char slot[TCLB_MIRROR_FIELDS];
+};
+
 constexpr int DIST_MAX_STAGES = 32;
 
 struct StagePlan {
@@ -83,6 +104,10 @@ struct StagePlan {
   int opb0, nopsb;
   int pk0, npk;     // pack ops (phase B)
   int run0, nruns;  // saved-field runs [runs[2i], runs[2i+1]) (copy-back of modes 1, 2)
+  int seg0;         // phase A segments: npack packs, then nunpack unpacks / pulls
+  int npack, nunpack;
+  int mir_lo, mir_hi;  // MirrorSpec of the low / high border launch (-1: none)
+  int yseg0, nyseg;    // IPC transport: the grid y phase's pulls (dir 3 segments)
 };
 
 struct SeriesEntry {
@@ -113,6 +138,8 @@ struct PartPlan {
   int integrate;             // 1: SimplePart rigid step after the stage (not in Init)
   int allreduce;             // 1: sum the accumulator over the ranks after the stage
   int reserved;
+  void* accbuf;              // IPC transport: this rank's shared copy of the accumulator
+  const double* const* accs; // and every rank's, mapped (device array of nranks pointers)
 };
 
 struct LoopPlan {
@@ -125,6 +152,9 @@ struct LoopPlan {
   const HaloOp* ops;
   const PackOp* packs;
   const int* runs;
+  const SegOp* segs;       // phase A segments (host)
+  const SegOp* dsegs;      // the same on the device (GPU copy kernels)
+  const MirrorSpec* mirrors;
   void* scratch;    // scratch snapshot (modes 1, 2)
   void* staging;    // staging buffer of the grid's y phase
   long long fs_bytes;  // bytes between field planes of a snapshot
@@ -136,6 +166,10 @@ struct LoopPlan {
   double* zonal;           // device zonal table (Launch.zonal)
   SamplePlan* samplers;    // host array of nsamplers plans (device buffers inside)
   PartPlan* part;          // null: no particles
+  // IPC transport: the neighbours' staging buffers mapped into this process (peer 0 / 1:
+  // below / above along the slab axis or the grid's z, 2 / 3: the grid's y) and their ranks
+  const void* peer_stg[4];
+  int ipc_peer[4];
 };
 
 typedef int (*run_fn)(const Launch*, int);
@@ -170,6 +204,20 @@ inline int dist_self_pairs(char* base, char* staging, const HaloOp* ops, int nop
   return 0;
 }
 
+// a border launch whose stores of the exchanged fields also land in the packed send
+// buffer (MirrorSpec m of the plan; m < 0: a plain launch)
+template <class S>
+inline int loop_run_mirrored(S& sv, Launch& L, const LoopPlan& P, int m) {
+  if (m < 0 || P.mirrors == nullptr) return sv.run(L);
+  const MirrorSpec& M = P.mirrors[m];
+  L.mbase = (char*)P.staging + M.boff;
+  L.mfs = M.mfs, L.msy = M.msy, L.msz = M.msz, L.moy = M.moy, L.moz = M.moz;
+  for (int i = 0; i < TCLB_MIRROR_FIELDS; i++) L.mslot[i] = M.slot[i];
+  const int r = sv.run(L);
+  L.mbase = nullptr;
+  return r;
+}
+
 // one launch over the whole local box
 template <class S>
 inline int loop_full(S& sv, Launch& L, const LoopPlan& P, int nx) {
@@ -187,38 +235,39 @@ inline int loop_full(S& sv, Launch& L, const LoopPlan& P, int nx) {
 template <class S>
 inline int loop_stage_plain(S& sv, Launch& L, const LoopPlan& P, const StagePlan& st, char* out, int nx) {
   int r;
-  const bool xch = (st.nops + st.nopsb) > 0;
+  const bool xch = (st.nops + st.nopsb + st.nunpack) > 0;
   if (!xch) return loop_full(sv, L, P, nx);
   if (P.axis == 3) {
     const int ny = P.ny, nz = P.nz, gy = P.gy, gz = P.gz;
     if (P.overlap && ny > 2 * gy && nz > 2 * gz) {
       const int box[4][4] = {{0, ny, 0, gz}, {0, ny, nz - gz, nz}, {0, gy, gz, nz - gz}, {ny - gy, ny, gz, nz - gz}};
+      const int mir[4] = {st.mir_lo, st.mir_hi, -1, -1};
       for (int b = 0; b < 4; b++) {
         L.ylo = box[b][0], L.yhi = box[b][1], L.zlo = box[b][2], L.zhi = box[b][3];
-        if ((r = sv.run(L)) != 0) return r;
+        if ((r = loop_run_mirrored(sv, L, P, mir[b])) != 0) return r;
       }
-      if ((r = sv.xstart(out, P, st)) != 0) return r;
+      if ((r = sv.xstart(out, P, st, 1)) != 0) return r;
       L.ylo = gy, L.yhi = ny - gy, L.zlo = gz, L.zhi = nz - gz;
       if ((r = sv.run(L)) != 0) return r;
       return sv.xfinish();
     }
     if ((r = loop_full(sv, L, P, nx)) != 0) return r;
-    if ((r = sv.xstart(out, P, st)) != 0) return r;
+    if ((r = sv.xstart(out, P, st, 0)) != 0) return r;
     return sv.xfinish();
   }
   const int n = P.n, g = P.g, ax = P.axis;
   if (P.overlap && n > 2 * g) {
     loop_set_range(L, ax, 0, g);
-    if ((r = sv.run(L)) != 0) return r;
+    if ((r = loop_run_mirrored(sv, L, P, st.mir_lo)) != 0) return r;
     loop_set_range(L, ax, n - g, n);
-    if ((r = sv.run(L)) != 0) return r;
-    if ((r = sv.xstart(out, P, st)) != 0) return r;
+    if ((r = loop_run_mirrored(sv, L, P, st.mir_hi)) != 0) return r;
+    if ((r = sv.xstart(out, P, st, 1)) != 0) return r;
     loop_set_range(L, ax, g, n - g);
     if ((r = sv.run(L)) != 0) return r;
     return sv.xfinish();
   }
   if ((r = loop_full(sv, L, P, nx)) != 0) return r;
-  if ((r = sv.xstart(out, P, st)) != 0) return r;
+  if ((r = sv.xstart(out, P, st, 0)) != 0) return r;
   return sv.xfinish();
 }
 
@@ -230,8 +279,8 @@ inline int loop_stage_oop(S& sv, Launch& L, const LoopPlan& P, const StagePlan& 
   L.out = P.scratch;
   if ((r = loop_full(sv, L, P, nx)) != 0) return r;
   if ((r = sv.copy_runs(out, P.scratch, P, st)) != 0) return r;
-  if (st.nops + st.nopsb > 0) {
-    if ((r = sv.xstart(out, P, st)) != 0) return r;
+  if (st.nops + st.nopsb + st.nunpack > 0) {
+    if ((r = sv.xstart(out, P, st, 0)) != 0) return r;
     if ((r = sv.xfinish()) != 0) return r;
   }
   L.out = out;

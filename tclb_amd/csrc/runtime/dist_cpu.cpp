@@ -76,10 +76,20 @@ struct CpuSvc {
     }
   }
 
-  int xstart(char* base, const tclb::LoopPlan& P, const tclb::StagePlan& st) {
+  void segcopy(char* base, char* stg, const tclb::LoopPlan& P, int s0, int n) {
+    for (int i = 0; i < n; i++) {
+      const tclb::SegOp& o = P.segs[s0 + i];
+      if (o.dir == 0) memcpy(stg + o.dst, base + o.src, (size_t)o.bytes);
+      else memcpy(base + o.dst, stg + o.src, (size_t)o.bytes);
+    }
+  }
+
+  int xstart(char* base, const tclb::LoopPlan& P, const tclb::StagePlan& st, int mirrored) {
     int r;
     char* stg = (char*)P.staging;
+    if (!mirrored) segcopy(base, stg, P, st.seg0, st.npack);
     if ((r = p2p(base, stg, P.ops + st.op0, st.nops)) != 0) return r;
+    segcopy(base, stg, P, st.seg0 + st.npack, st.nunpack);
     if (st.nopsb > 0) {
       packs(base, stg, P.packs + st.pk0, st.npk, 0);
       if ((r = p2p(base, stg, P.ops + st.opb0, st.nopsb)) != 0) return r;
@@ -156,5 +166,7 @@ int tclb_loop_sizeof_part_cpu() { return (int)sizeof(tclb::PartPlan); }
 int tclb_loop_sizeof_pack_cpu() { return (int)sizeof(tclb::PackOp); }
 int tclb_loop_sizeof_series_cpu() { return (int)sizeof(tclb::SeriesEntry); }
 int tclb_dist_sizeof_op_cpu() { return (int)sizeof(tclb::HaloOp); }
+int tclb_loop_sizeof_seg_cpu() { return (int)sizeof(tclb::SegOp); }
+int tclb_loop_sizeof_mirror_cpu() { return (int)sizeof(tclb::MirrorSpec); }
 
 }  // extern "C"

@@ -558,6 +558,10 @@ class Lattice:
 
     def exchange(self, buf: Optional[torch.Tensor] = None, fields=None):
         buf = self.snaps[self.cur] if buf is None else buf
+        if self._dist is not None and self._dist.gpu and self._dist.transport == "ipc":
+            # the IPC ranks' halos only travel through the native loop's transport
+            self._dist.exchange_fields(buf, fields)
+            return
         self._halo_finish(self._halo_start(buf, fields))
 
     # ------------------------------------------------------------------ actions

@@ -54,9 +54,21 @@ class PackOp(ctypes.Structure):
                 ("unpack", ctypes.c_int), ("reserved", ctypes.c_int)]
 
 
+class SegOp(ctypes.Structure):
+    _fields_ = [("dst", ctypes.c_longlong), ("src", ctypes.c_longlong), ("bytes", ctypes.c_longlong),
+                ("dir", ctypes.c_int), ("peer", ctypes.c_int)]
+
+
+class MirrorSpec(ctypes.Structure):
+    _fields_ = [("boff", ctypes.c_longlong), ("mfs", ctypes.c_longlong), ("msy", ctypes.c_longlong),
+                ("msz", ctypes.c_longlong), ("moy", ctypes.c_int), ("moz", ctypes.c_int),
+                ("slot", ctypes.c_byte * abi.MIRROR_FIELDS)]
+
+
 class StagePlan(ctypes.Structure):
     _fields_ = [(k, ctypes.c_int) for k in ("stage", "mode", "sweeps", "particle", "op0", "nops", "opb0", "nopsb",
-                                            "pk0", "npk", "run0", "nruns")]
+                                            "pk0", "npk", "run0", "nruns", "seg0", "npack", "nunpack", "mir_lo",
+                                            "mir_hi", "yseg0", "nyseg")]
 
 
 class SeriesEntry(ctypes.Structure):
@@ -70,7 +82,8 @@ class PartPlan(ctypes.Structure):
                 ("ncell", ctypes.c_int), ("nl", ctypes.c_int), ("mscale", ctypes.c_double),
                 ("tmp", ctypes.c_void_p), ("tmp_bytes", ctypes.c_longlong), ("a", ctypes.c_double * 3),
                 ("period", ctypes.c_double * 3), ("periodic", ctypes.c_int), ("integrate", ctypes.c_int),
-                ("allreduce", ctypes.c_int), ("reserved", ctypes.c_int)]
+                ("allreduce", ctypes.c_int), ("reserved", ctypes.c_int), ("accbuf", ctypes.c_void_p),
+                ("accs", ctypes.c_void_p)]
 
 
 class LoopPlan(ctypes.Structure):
@@ -78,18 +91,21 @@ class LoopPlan(ctypes.Structure):
                 ("ny", ctypes.c_int), ("nz", ctypes.c_int), ("gy", ctypes.c_int), ("gz", ctypes.c_int),
                 ("overlap", ctypes.c_int), ("nstages", ctypes.c_int), ("st", StagePlan * MAX_STAGES),
                 ("ops", ctypes.c_void_p), ("packs", ctypes.c_void_p), ("runs", ctypes.c_void_p),
+                ("segs", ctypes.c_void_p), ("dsegs", ctypes.c_void_p), ("mirrors", ctypes.c_void_p),
                 ("scratch", ctypes.c_void_p), ("staging", ctypes.c_void_p), ("fs_bytes", ctypes.c_longlong),
                 ("nseries", ctypes.c_int), ("nsamplers", ctypes.c_int), ("series", ctypes.c_void_p),
                 ("svals", ctypes.c_void_p), ("sslopes", ctypes.c_void_p), ("zonal", ctypes.c_void_p),
-                ("samplers", ctypes.c_void_p), ("part", ctypes.c_void_p)]
+                ("samplers", ctypes.c_void_p), ("part", ctypes.c_void_p), ("peer_stg", ctypes.c_void_p * 4),
+                ("ipc_peer", ctypes.c_int * 4)]
 
 
 XCHG_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(HaloOp),
                            ctypes.c_int)
 ALLRED_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_longlong)
 
-TRANSPORT_CODE = {"copy": 0, "rccl": 1, "callback": 2}
-_SIZES = (("plan", LoopPlan), ("stage", StagePlan), ("part", PartPlan), ("pack", PackOp), ("series", SeriesEntry))
+TRANSPORT_CODE = {"copy": 0, "rccl": 1, "callback": 2, "ipc": 3}
+_SIZES = (("plan", LoopPlan), ("stage", StagePlan), ("part", PartPlan), ("pack", PackOp), ("series", SeriesEntry),
+          ("seg", SegOp), ("mirror", MirrorSpec))
 
 
 class NativeDistError(RuntimeError):
@@ -143,12 +159,26 @@ def _dev_lib():
         L.tclb_loop_iterate.restype = i
         L.tclb_ad_segment.argtypes = [P, P, P]
         L.tclb_ad_segment.restype = i
+        L.tclb_loop_exchange.argtypes = [P, P, P, i, i, ctypes.c_longlong, ctypes.c_longlong, ctypes.c_longlong, i, P]
+        L.tclb_loop_exchange.restype = i
         L.tclb_dist_exchange.argtypes = [P, P, P, i, P]
         L.tclb_dist_exchange.restype = i
         L.tclb_dist_wait.argtypes = [P, P, i]
         L.tclb_dist_wait.restype = i
         L.tclb_part_tmp_bytes.argtypes = [i, i]
         L.tclb_part_tmp_bytes.restype = ctypes.c_longlong
+        L.tclb_ipc_alloc.argtypes = [ctypes.c_longlong, P]
+        L.tclb_ipc_alloc.restype = P
+        L.tclb_ipc_free.argtypes = [P]
+        L.tclb_ipc_open.argtypes = [P]
+        L.tclb_ipc_open.restype = P
+        L.tclb_ipc_close.argtypes = [P]
+        L.tclb_dist_sig_handle.argtypes = [P, P]
+        L.tclb_dist_sig_handle.restype = i
+        L.tclb_dist_sig_attach.argtypes = [P, ctypes.c_char_p]
+        L.tclb_dist_sig_attach.restype = i
+        L.tclb_dist_ipc_error.argtypes = [P]
+        L.tclb_dist_ipc_error.restype = i
         for name, st in _SIZES:
             if getattr(L, f"tclb_loop_sizeof_{name}")() != ctypes.sizeof(st):
                 raise NativeDistError(f"ABI mismatch of the loop {name} struct in libtclb_device.so")
@@ -163,15 +193,19 @@ def _err() -> str:
 
 
 def choose_transport(comm, gpu: bool) -> str:
+    """GPU ranks: RCCL (default) or IPC (TCLB_DIST_TRANSPORT=ipc, or a gloo process group:
+    several processes on one device, which RCCL refuses); CPU ranks: gloo callbacks; one
+    rank: device copies, or RCCL / IPC to itself when asked (the multi-rank code on one
+    GPU)"""
     env = os.environ.get("TCLB_DIST_TRANSPORT", "auto")
     if isinstance(comm, TorchDistComm):
         if gpu:
-            if comm.backend != "nccl":
-                raise NativeDistError(f"native GPU loop needs the nccl (RCCL) backend, not {comm.backend}")
+            if env == "ipc" or comm.backend != "nccl":
+                return "ipc"
             return "rccl"
         return "callback"
-    if env == "rccl" and gpu:
-        return "rccl"          # one rank, RCCL send/receive to itself
+    if env in ("rccl", "ipc") and gpu:
+        return env             # one rank sending to / pulling from itself
     return "copy"
 
 
@@ -197,10 +231,53 @@ def gpu_context(comm, transport: str, device: torch.device) -> int:
                 ctypes.memmove(uid, raw, 128)
         with torch.cuda.device(device):
             ctx = L.tclb_dist_ctx_create(path, TRANSPORT_CODE[transport], size, rank, uid)
-        if not ctx:
-            raise NativeDistError(f"native dist context ({transport}) failed: {_err()}")
+            if not ctx:
+                raise NativeDistError(f"native dist context ({transport}) failed: {_err()}")
+            if transport == "ipc":
+                # every rank maps every other rank's signal block (counters of the pulls)
+                hb = ctypes.create_string_buffer(HANDLE_BYTES)
+                if L.tclb_dist_sig_handle(ctx, hb) != 0:
+                    raise NativeDistError(f"IPC signal handle failed: {_err()}")
+                hs = comm.gather_objects(bytes(hb.raw)) if size > 1 else [bytes(hb.raw)]
+                if L.tclb_dist_sig_attach(ctx, b"".join(hs)) != 0:
+                    raise NativeDistError(f"IPC signal attach failed: {_err()}")
         _ctx_cache[key] = ctx
         return ctx
+
+
+HANDLE_BYTES = 64     # hipIpcMemHandle_t
+
+
+class IpcBuf:
+    """device memory another process of the node can map (tclb_ipc_alloc: zeroed)"""
+
+    def __init__(self, nbytes: int, device: torch.device):
+        self.handle = ctypes.create_string_buffer(HANDLE_BYTES)
+        with torch.cuda.device(device):
+            self.ptr = _dev_lib().tclb_ipc_alloc(int(nbytes), self.handle)
+        if not self.ptr:
+            raise NativeDistError(f"IPC buffer of {nbytes} bytes: {_err()}")
+        self.nbytes = int(nbytes)
+
+    def __del__(self):
+        if getattr(self, "ptr", None) and _dev is not None:
+            _dev.tclb_ipc_free(self.ptr)
+            self.ptr = None
+
+
+class IpcMap:
+    """another rank's IpcBuf mapped into this process"""
+
+    def __init__(self, handle: bytes, device: torch.device):
+        with torch.cuda.device(device):
+            self.ptr = _dev_lib().tclb_ipc_open(handle)
+        if not self.ptr:
+            raise NativeDistError(f"IPC open failed: {_err()}")
+
+    def __del__(self):
+        if getattr(self, "ptr", None) and _dev is not None:
+            _dev.tclb_ipc_close(self.ptr)
+            self.ptr = None
 
 
 def _runs(idx: List[int]) -> List[Tuple[int, int]]:
@@ -242,7 +319,7 @@ class NativeLoop:
         self._cb = XCHG_FN(self._exchange_cb) if cb else None
         self._ared = ALLRED_FN(self._allreduce_cb) if cb else None
         self._cb_error: Optional[str] = None
-        self._staging: Optional[torch.Tensor] = None
+        self._staging: Dict[int, torch.Tensor] = {}     # data_ptr -> the plans' staging buffers
         self._part_tmp: Optional[torch.Tensor] = None
 
     @staticmethod
@@ -284,11 +361,85 @@ class NativeLoop:
             ops.append(((f * lat.fs + (n + g) * plane) * es, b, 1, nxt, TAG_HI + f, 0))
         return ops
 
-    def y_phase(self, fields, stg_off: int):
-        """the grid's y phase of one stage: rows [n, n+g) of the fields read from below go
+    def phase_a(self, fields, stg_off: int, k: int = 0, lay=None, peer_off=None):
+        """the packed exchange of stage k along the slab axis (or the z phase of the
+        grid): ONE message per neighbour and direction.  The border launches mirror their
+        stores of the exchanged fields into the send buffers (MirrorSpec; a launch that
+        cannot — no overlap split, out-of-place stages — is followed by pack segments), the
+        received buffers are unpacked into the ghost planes by one copy launch.  Staging
+        layout [send up][send down][recv below][recv above], each [field][g planes]; the
+        copy transport (this rank is its own neighbour) receives nothing: its send buffers
+        are unpacked directly; the IPC transport receives nothing either: it pulls the
+        neighbours' send buffers straight into its ghost planes (dir 2 segments, source
+        offsets from the neighbour's own layout, peer_off).  Ops in the issue order every
+        rank shares: send up, send down, receive from below, receive from above.  Returns
+        (ops, packs, unpacks, mirrors (lo launch, hi launch), staging bytes)."""
+        lat = self.lat
+        grid = lat.slab.axis == 3
+        ax = 2 if grid else lat.slab.axis
+        g = lat.gz if grid else lat.g
+        n = lat.shape[2] if ax == 2 else lat.shape[1]
+        plane = lat.NY * lat.px if ax == 2 else lat.px
+        es = lat.snaps[0].element_size()
+        prev, nxt = self._peers(ax)
+        fs = set(fields)
+        lo_set, hi_set = lat.halo_sets[ax]
+        lo = [i for i in lo_set if i in fs]        # read from below: my top planes go up
+        hi = [i for i in hi_set if i in fs]        # read from above: my bottom planes go down
+        per = g * plane * es
+        off = stg_off
+        su, off = off, off + per * len(lo)
+        sd, off = off, off + per * len(hi)
+        if lay is not None:
+            lay[(k, "A_su")], lay[(k, "A_sd")] = su, sd
+        ipc = self.transport == "ipc"
+        if self.transport == "copy":
+            rb, ra = su, sd
+        elif not ipc:
+            rb, off = off, off + per * len(lo)
+            ra, off = off, off + per * len(hi)
+        ops = []
+        if self.transport not in ("copy", "ipc"):
+            if lo:
+                ops.append((su, per * len(lo), 0, nxt, 0, 1))
+            if hi:
+                ops.append((sd, per * len(hi), 0, prev, TAG_HI, 1))
+            if lo:
+                ops.append((rb, per * len(lo), 1, prev, 0, 1))
+            if hi:
+                ops.append((ra, per * len(hi), 1, nxt, TAG_HI, 1))
+        fsb = lat.fs * es
+        packs = [(su + j * per, f * fsb + n * plane * es, per, 0, 0) for j, f in enumerate(lo)] + \
+                [(sd + j * per, f * fsb + g * plane * es, per, 0, 0) for j, f in enumerate(hi)]
+        if ipc:
+            pu = peer_off(0, k, "A_su") if lo else 0      # the rank below's send-up buffer
+            pd = peer_off(1, k, "A_sd") if hi else 0      # the rank above's send-down buffer
+            unpacks = [(f * fsb, pu + j * per, per, 2, 0) for j, f in enumerate(lo)] + \
+                      [(f * fsb + (n + g) * plane * es, pd + j * per, per, 2, 1) for j, f in enumerate(hi)]
+        else:
+            unpacks = [(f * fsb, rb + j * per, per, 1, 0) for j, f in enumerate(lo)] + \
+                      [(f * fsb + (n + g) * plane * es, ra + j * per, per, 1, 0) for j, f in enumerate(hi)]
+
+        def mirror(flist, boff, r0):
+            if not flist:
+                return None
+            slot = [-1] * abi.MIRROR_FIELDS
+            for j, f in enumerate(flist):
+                slot[f] = j
+            if ax == 2:
+                spec = (g * plane, lat.px, lat.NY * lat.px, lat.gy, -r0)
+            else:
+                spec = (g * plane, lat.px, g * lat.px, -r0, lat.gz)
+            return (boff,) + spec + (slot,)
+        mirrors = (mirror(hi, sd, 0), mirror(lo, su, n - g))
+        return ops, packs, unpacks, mirrors, off - stg_off
+
+    def y_phase(self, fields, stg_off: int, k: int = 0, lay=None, peer_off=None):
+        """the grid's y phase of stage k: rows [n, n+g) of the fields read from below go
         up, rows [g, 2g) of those read from above go down, over the ghost-inclusive z
         extent, through staging messages [send up][send down][recv below][recv above];
-        returns (ops, packs, bytes)"""
+        the IPC transport pulls the y neighbours' send messages into its receive buffers
+        (dir 3 segments) instead of exchanging them.  Returns (ops, packs, pulls, bytes)"""
         lat = self.lat
         g, n = lat.gy, lat.shape[1]
         es = lat.snaps[0].element_size()
@@ -298,11 +449,14 @@ class NativeLoop:
         lo = [i for i in lo_set if i in fs]
         hi = [i for i in hi_set if i in fs]
         per = lat.NZ * g * lat.px * es             # one field's rows
-        ops, packs = [], []
+        ops, packs, pulls = [], [], []
         msgs, off = {}, stg_off
         for name, flist in (("su", lo), ("sd", hi), ("rb", lo), ("ra", hi)):
             msgs[name] = off
             off += per * len(flist)
+        if lay is not None:
+            lay[(k, "B_su")], lay[(k, "B_sd")] = msgs["su"], msgs["sd"]
+        ipc = self.transport == "ipc"
 
         def pk(base, flist, y0, unpack):
             o = base
@@ -312,17 +466,25 @@ class NativeLoop:
                 o += per * (r1 - r0)
         if lo:
             pk(msgs["su"], lo, n, 0)
-            ops.append((msgs["su"], per * len(lo), 0, nxt, TAG_Y, 1))
+            if not ipc:
+                ops.append((msgs["su"], per * len(lo), 0, nxt, TAG_Y, 1))
         if hi:
             pk(msgs["sd"], hi, g, 0)
-            ops.append((msgs["sd"], per * len(hi), 0, prev, TAG_Y + TAG_HI, 1))
+            if not ipc:
+                ops.append((msgs["sd"], per * len(hi), 0, prev, TAG_Y + TAG_HI, 1))
         if lo:
-            ops.append((msgs["rb"], per * len(lo), 1, prev, TAG_Y, 1))
+            if ipc:
+                pulls.append((msgs["rb"], peer_off(2, k, "B_su"), per * len(lo), 3, 2))
+            else:
+                ops.append((msgs["rb"], per * len(lo), 1, prev, TAG_Y, 1))
             pk(msgs["rb"], lo, 0, 1)
         if hi:
-            ops.append((msgs["ra"], per * len(hi), 1, nxt, TAG_Y + TAG_HI, 1))
+            if ipc:
+                pulls.append((msgs["ra"], peer_off(3, k, "B_sd"), per * len(hi), 3, 3))
+            else:
+                ops.append((msgs["ra"], per * len(hi), 1, nxt, TAG_Y + TAG_HI, 1))
             pk(msgs["ra"], hi, n + g, 1)
-        return ops, packs, off - stg_off
+        return ops, packs, pulls, off - stg_off
 
     @staticmethod
     def stage_mode(k: int, st) -> int:
@@ -333,14 +495,71 @@ class NativeLoop:
             return 1
         return 0
 
-    def plan(self, action: str):
+    def _ipc_ranks(self) -> List[int]:
+        """ranks of the IPC peers 0..3: below / above along the slab axis (the grid's z),
+        then below / above along the grid's y (-1: none)"""
+        lat = self.lat
+        if lat.g == 0:
+            return [-1] * 4
+        if lat.slab.axis == 3:
+            return list(self._peers(2)) + list(self._peers(1))
+        return list(self._peers(lat.slab.axis)) + [-1, -1]
+
+    def _build(self, P: LoopPlan, stages, lay, peer_off, field_lists=None):
+        """fill P's stages (field_lists: exchange-only stages of these field sets);
+        returns (ops, packs, runs, segs, mirrors, staging bytes, needs the scratch
+        snapshot)"""
         lat = self.lat
         m = lat.model
-        key = (action, lat.g, lat.overlap)
+        ax = P.axis
+        allops, allpacks, runs, segs, mirrors = [], [], [], [], []
+        stg_bytes = 0
+        need_scratch = False
+        for k, si in enumerate(stages):
+            st = m.stages[si]
+            fields = lat._saved_fields(st) if field_lists is None else field_lists[k]
+            mode = self.stage_mode(k, st) if field_lists is None else 0
+            need_scratch |= mode > 0
+            S = P.st[k]
+            S.stage, S.mode, S.sweeps = si, mode, FIXED_POINT_SWEEPS if mode == 2 else 1
+            S.particle = 1 if st.particle and field_lists is None else 0
+            S.run0, S.nruns = len(runs), len(_runs(fields)) if mode > 0 else 0
+            if mode > 0:
+                runs += _runs(fields)
+            S.mir_lo = S.mir_hi = -1
+            if ax > 0:
+                ops, pks, ups, mirs, nb = self.phase_a(fields, stg_bytes, k, lay, peer_off)
+                stg_bytes += nb
+                S.op0, S.nops = len(allops), len(ops)
+                allops += ops
+                S.seg0, S.npack, S.nunpack = len(segs), len(pks), len(ups)
+                segs += pks + ups
+                for side, mspec in zip(("mir_lo", "mir_hi"), mirs):
+                    if mspec is not None:
+                        setattr(S, side, len(mirrors))
+                        mirrors.append(mspec)
+                if ax == 3:
+                    yops, ypk, ypull, yb = self.y_phase(fields, stg_bytes, k, lay, peer_off)
+                    S.opb0, S.nopsb = len(allops), len(yops)
+                    S.pk0, S.npk = len(allpacks), len(ypk)
+                    S.yseg0, S.nyseg = len(segs), len(ypull)
+                    segs += ypull
+                    allops += yops
+                    allpacks += ypk
+                    stg_bytes += yb
+        return allops, allpacks, runs, segs, mirrors, stg_bytes, need_scratch
+
+    def plan(self, action: str, fields: Optional[Tuple[int, ...]] = None):
+        """the loop plan of `action` (cached); fields: instead a one-stage plan that only
+        exchanges these fields (exchange_fields)"""
+        lat = self.lat
+        m = lat.model
+        key = (action, lat.g, lat.overlap, fields)
         p = self._plans.get(key)
         if p is not None:
             return p
-        stages = [m.stage_index(s) for s in m.action(action).stages]
+        stages = [m.stage_index(s) for s in m.action(action).stages] if fields is None else [0]
+        flists = None if fields is None else [list(fields)]
         if len(stages) > MAX_STAGES:
             raise NativeDistError(f"action of {len(stages)} stages (max {MAX_STAGES})")
         P = LoopPlan()
@@ -353,31 +572,36 @@ class NativeLoop:
         elif ax == 3:
             P.ny, P.nz, P.gy, P.gz = lat.shape[1], lat.shape[2], lat.gy, lat.gz
         P.nstages = len(stages)
-        allops, allpacks, runs = [], [], []
-        stg_bytes = 0
-        need_scratch = False
-        for k, si in enumerate(stages):
-            st = m.stages[si]
-            fields = lat._saved_fields(st)
-            mode = self.stage_mode(k, st)
-            need_scratch |= mode > 0
-            S = P.st[k]
-            S.stage, S.mode, S.sweeps = si, mode, FIXED_POINT_SWEEPS if mode == 2 else 1
-            S.particle = 1 if st.particle else 0
-            S.run0, S.nruns = len(runs), len(_runs(fields)) if mode > 0 else 0
-            if mode > 0:
-                runs += _runs(fields)
-            if ax > 0:
-                ops = self.ops_for(fields)
-                S.op0, S.nops = len(allops), len(ops)
-                allops += ops
-                if ax == 3:
-                    yops, ypk, yb = self.y_phase(fields, stg_bytes)
-                    S.opb0, S.nopsb = len(allops), len(yops)
-                    S.pk0, S.npk = len(allpacks), len(ypk)
-                    allops += yops
-                    allpacks += ypk
-                    stg_bytes += yb
+        keep: list = []
+        ipc = self.transport == "ipc" and ax > 0
+        peer_off = None
+        if ipc:
+            # two passes: this rank's staging layout, then (its buffer allocated and every
+            # rank's layout and handle gathered) the pulls from the neighbours' layouts
+            lay: Dict[tuple, int] = {}
+            nb = self._build(P, stages, lay, lambda *a: 0, flists)[5]
+            buf = IpcBuf(max(nb, 16), lat.device)
+            keep.append(buf)
+            mine = (lay, bytes(buf.handle.raw))
+            every = lat.comm.gather_objects(mine) if self.multi else [mine]
+            ranks = self._ipc_ranks()
+            maps: Dict[int, int] = {}
+            for r in ranks:
+                if r >= 0 and r not in maps:
+                    if r == self.rank:
+                        maps[r] = buf.ptr
+                    else:
+                        mp_ = IpcMap(every[r][1], lat.device)
+                        keep.append(mp_)
+                        maps[r] = mp_.ptr
+            for i, r in enumerate(ranks):
+                P.ipc_peer[i] = r
+                P.peer_stg[i] = maps[r] if r >= 0 else None
+            peer_off = lambda i, k, name: every[ranks[i]][0][(k, name)]  # noqa: E731
+        else:
+            for i in range(4):
+                P.ipc_peer[i] = -1
+        allops, allpacks, runs, segs, mirrors, stg_bytes, need_scratch = self._build(P, stages, None, peer_off, flists)
         arr = _carr(HaloOp, [dict(zip(_OPF, o)) for o in allops])
         pks = _carr(PackOp, allpacks)
         rarr = (ctypes.c_int * max(2, 2 * len(runs)))(*[v for r in runs for v in r])
@@ -385,14 +609,34 @@ class NativeLoop:
         P.packs = ctypes.cast(pks, ctypes.c_void_p)
         P.runs = ctypes.cast(rarr, ctypes.c_void_p)
         P.fs_bytes = lat.fs * lat.snaps[0].element_size()
-        keep = [arr, pks, rarr]
+        sarr = _carr(SegOp, [dict(zip(("dst", "src", "bytes", "dir", "peer"), o)) for o in segs])
+        marr = (MirrorSpec * max(1, len(mirrors)))()
+        for i, (boff, mfs, msy, msz, moy, moz, slot) in enumerate(mirrors):
+            M = marr[i]
+            M.boff, M.mfs, M.msy, M.msz, M.moy, M.moz = boff, mfs, msy, msz, moy, moz
+            M.slot[:] = slot
+        P.segs = ctypes.cast(sarr, ctypes.c_void_p)
+        P.mirrors = ctypes.cast(marr, ctypes.c_void_p)
+        keep += [arr, pks, rarr, sarr, marr]
+        if self.gpu and segs:
+            dsg = torch.frombuffer(bytearray(bytes(sarr)), dtype=torch.uint8).to(lat.device)
+            keep.append(dsg)
+            P.dsegs = dsg.data_ptr()
+        else:
+            P.dsegs = P.segs
         if need_scratch:
             sc = lat._scratch_snapshot()
             P.scratch = sc.data_ptr()
-        if stg_bytes:
-            if self._staging is None or self._staging.numel() < stg_bytes:
-                self._staging = torch.zeros(stg_bytes, dtype=torch.uint8, device=lat.device)
-            P.staging = self._staging.data_ptr()
+        if ipc:
+            P.staging = keep[0].ptr
+        elif stg_bytes:
+            # each plan owns its staging buffer (kept alive with the plan): a buffer shared
+            # by the cached plans and regrown for a larger one would leave the earlier
+            # plans' raw pointers dangling
+            stg = torch.zeros(stg_bytes, dtype=torch.uint8, device=lat.device)
+            keep.append(stg)
+            P.staging = stg.data_ptr()
+            self._staging[P.staging] = stg
         p = self._plans[key] = (P, keep)
         return p
 
@@ -472,8 +716,31 @@ class NativeLoop:
                 Q.a[k], Q.period[k] = float(integ["a"][k]), float(integ["period"][k])
             Q.periodic = int(integ["periodic"])
         Q.allreduce = 1 if (lat.comm.distributed and lat.comm.size > 1) else 0
+        if Q.allreduce and self.gpu and self.transport == "ipc":
+            Q.accbuf, Q.accs = self._ipc_acc(max(n, 1))
         keep.append(Q)
         P.part = ctypes.cast(ctypes.pointer(Q), ctypes.c_void_p)
+
+    def _ipc_acc(self, n: int):
+        """the IPC all-reduce of the particle forces: this rank's shared copy of the
+        accumulator and a device table of every rank's (collective on first use and when
+        the particle count grows — the count is global, so every rank grows together)"""
+        cur = getattr(self, "_acc_ipc", None)
+        if cur is None or cur[0] < n:
+            lat = self.lat
+            buf = IpcBuf(48 * n, lat.device)
+            hs = lat.comm.gather_objects(bytes(buf.handle.raw))
+            maps, ptrs = [], []
+            for r, h in enumerate(hs):
+                if r == self.rank:
+                    ptrs.append(buf.ptr)
+                else:
+                    mp_ = IpcMap(h, lat.device)
+                    maps.append(mp_)
+                    ptrs.append(mp_.ptr)
+            tab = torch.tensor(ptrs, dtype=torch.int64, device=lat.device)
+            self._acc_ipc = cur = (n, buf, maps, tab)
+        return cur[1].ptr, cur[3].data_ptr()
 
     # ------------------------------------------------------------------ run
     def iterate(self, L: abi.Launch, n: int, action: str, glob_last: bool):
@@ -510,13 +777,28 @@ class NativeLoop:
     def wait(self, timeout_ms: Optional[int] = None):
         """wait for this rank's queued work with the RCCL communicator watched (a dead peer
         aborts the communicator and raises instead of hanging the rank)"""
-        if not self.gpu or self.transport != "rccl":
+        if not self.gpu or self.transport not in ("rccl", "ipc"):
             return
         t = int(os.environ.get("TCLB_DIST_TIMEOUT_MS", "600000")) if timeout_ms is None else timeout_ms
         stream = torch.cuda.current_stream(self.lat.device).cuda_stream
         r = _dev_lib().tclb_dist_wait(self.ctx, stream, t)
         if r != 0:
             raise NativeDistError(f"native loop wait failed ({r}): {_err()}")
+
+    def exchange_fields(self, buf: torch.Tensor, fields=None):
+        """one halo exchange of `fields` (None: all) of snapshot `buf` through the loop's
+        own plan and transport (GPU ranks: RCCL or IPC); collective"""
+        lat = self.lat
+        fl = tuple(range(lat.nf)) if fields is None else tuple(sorted(set(fields)))
+        P, _ = self.plan("Iteration", fl)
+        if P.axis == 0:
+            return
+        stream = torch.cuda.current_stream(lat.device).cuda_stream
+        L = lat._L
+        r = _dev_lib().tclb_loop_exchange(self.ctx, buf.data_ptr(), ctypes.byref(P), 0, buf.element_size(),
+                                          L.fs, L.sz, L.sy, L.px, stream)
+        if r != 0:
+            raise NativeDistError(f"native halo exchange failed ({r}): {_err()}")
 
     def exchange(self, buf: torch.Tensor, fields):
         """one exchange of `fields` of snapshot `buf` through the native transport (GPU)"""
@@ -544,7 +826,7 @@ class NativeLoop:
             d = comm.dist
             flat = self._flat(base)
             es = flat.element_size()
-            stg = self._staging
+            stg = self._staging.get(staging) if staging else None
             p2p = []
             # TCLB_DIST_ORDER_MATCH=1: pair sends and receives by issue order per peer (the
             # k-th send to a peer with that peer's k-th receive from us), ignoring the plan's

@@ -358,9 +358,16 @@ class SimplePart(ParticleSystem):
                 "periodic": sum(1 << k for k in range(3) if self.periodic[k])}
 
     def after_native(self, lat, n: int, action: str):
+        """bookkeeping after n native steps of `action`: the Python step path calls step()
+        once per particle stage per step (not in Init), so the iteration count advances by
+        n times the action's particle stages (0 when it has none)"""
         self._host_stale |= {"force", "torque"}
-        if action != "Init" and self.n:
-            self.iteration += n
+        if action == "Init":
+            return
+        m = lat.model
+        k = sum(1 for s in m.action(action).stages if m.stage(s).particle)
+        self.iteration += n * k
+        if k and self.n:
             self._host_stale |= {"x", "v", "omega"}
 
     def step(self, lat):

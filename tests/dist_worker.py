@@ -69,7 +69,16 @@ def worker(rank, world, port, model, shape, steps, out, overlap, grid=None, nati
     dist.destroy_process_group()
 
 
-def worker_catalog(rank, world, port, model, steps, out, overlap, mirror="1"):
+def alternate_actions(lat, steps):
+    """Iteration and TempToSteadyState alternately (two native plans with different
+    staging sizes on a Y x Z grid; ADVICE r05: a shared, regrown staging buffer left the
+    first plan pointing at freed memory)"""
+    for _ in range(steps):
+        lat.iterate(1, action="Iteration")
+        lat.iterate(1, glob_last=False, action="TempToSteadyState")
+
+
+def worker_catalog(rank, world, port, model, steps, out, overlap, mirror="1", alternate=False):
     """any catalog model with the generic set-up of tests/model_cases.py (global-coordinate
     perturbation), gathered to rank 0 as in worker()"""
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -84,7 +93,10 @@ def worker_catalog(rank, world, port, model, steps, out, overlap, mirror="1"):
     lat.overlap = lat.overlap and overlap
     lat.init()
     perturb(lat)
-    lat.iterate(steps)
+    if alternate:
+        alternate_actions(lat, steps)
+    else:
+        lat.iterate(steps)
     parts = comm.gather_objects((lat.slab.offset, lat.fields_interior().numpy(), lat.globals))
     if rank == 0:
         gnx, gny, gnz = lat.gshape

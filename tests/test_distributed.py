@@ -122,6 +122,44 @@ def test_yz_grid_matches_single(tmp_path, shape, world, grid):
         assert abs(g[k] - v) <= 1e-11 * (1 + abs(v)), k
 
 
+@pytest.mark.parametrize("shape,world,grid", [
+    ((16, 8, 12), 4, (2, 2)),
+    ((12, 9, 8), 6, (3, 2)),
+])
+def test_yz_grid_pairs_by_issue_order(tmp_path, monkeypatch, shape, world, grid):
+    """the Y x Z grid's native plan (packed z phase, staged y rows) with sends and receives
+    paired by issue order per peer, tags ignored (RCCL's grouped send/receive semantics),
+    equals one rank bit for bit"""
+    monkeypatch.setenv("TCLB_DIST_ORDER_MATCH", "1")
+    steps = 3
+    ref = dist_worker.run_case("d3q27", shape, steps, LoopbackComm())
+    out = str(tmp_path / "full.npy")
+    mp.start_processes(dist_worker.worker, args=(world, _port(), "d3q27", shape, steps, out, None, grid, "1"),
+                       nprocs=world, start_method="spawn", join=True)
+    assert open(out + ".axis").read() == "3"
+    assert np.array_equal(np.load(out), ref.fields_interior().numpy())
+    assert json.load(open(out + ".json"))["_native"] == "callback"
+
+
+def test_grid_alternating_actions(tmp_path, monkeypatch):
+    """a multi-stage model on a 2 x 2 grid alternating two actions whose native plans
+    have different staging sizes (Iteration / TempToSteadyState) equals one rank"""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from model_cases import make_case, perturb
+    model = "d3q27_pf_velocity_thermo"
+    ref = make_case(model, "cpu")
+    ref.init()
+    perturb(ref)
+    dist_worker.alternate_actions(ref, 2)
+    monkeypatch.setenv("TCLB_GRID", "2,2")
+    monkeypatch.setenv("TCLB_DIST_ORDER_MATCH", "1")
+    out = str(tmp_path / "full.npy")
+    mp.start_processes(dist_worker.worker_catalog, args=(4, _port(), model, 2, out, True, "1", True),
+                       nprocs=4, start_method="spawn", join=True)
+    assert np.array_equal(np.load(out), ref.fields_interior().numpy())
+
+
 def test_choose_grid_minimises_cut():
     from tclb_amd.parallel.decomp import choose_grid, decompose
     assert choose_grid(512, 512, 512, 8) in ((2, 4), (4, 2))

@@ -132,7 +132,7 @@ def main():
     ap.add_argument("--shape", default="", help="explicit lattice nx,ny,nz (overrides --size)")
     ap.add_argument("--loopback-dist", action="store_true",
                     help="one rank through the multi-rank path (a per-rank slab of an N-GPU run)")
-    ap.add_argument("--transport", default=None, choices=["rccl", "copy"])
+    ap.add_argument("--transport", default=None, choices=["rccl", "copy", "ipc"])
     a = ap.parse_args()
     if a.transport:
         os.environ["TCLB_DIST_TRANSPORT"] = a.transport
