@@ -9,16 +9,18 @@
 // advanced per iteration (:473-477), the samplers filled after each iteration (:1376-1389).
 //
 // Per stage k of the action (StagePlan.mode):
-//   0 plain      slab: the two border launches, then the halo exchange of the stage's
-//                saved fields starts on the transport (GPU: high-priority comm stream,
-//                ncclSend/ncclRecv of each field's planes STRAIGHT FROM / INTO the output
-//                snapshot — a field's planes are contiguous in the [field][z][y][x]
-//                layout, so no pack, unpack or staging buffer), then the interior launch
-//                concurrent with it; the compute stream waits for the exchange only before
-//                the next stage.  Y x Z grid: the four border boxes, then the two-phase
-//                exchange (z planes direct, then y rows over the ghost-inclusive z extent —
-//                which also fills the edge ghosts — packed into a staging buffer), then the
-//                interior box.  One rank without ghosts: one launch.
+//   0 plain      slab: the two border launches, whose stores of the exchanged fields
+//                also land in one packed send buffer per direction (MirrorSpec ->
+//                core.hpp mirror_store), then the halo exchange of the stage starts on the
+//                transport (GPU: high-priority comm stream; ONE message per neighbour and
+//                direction, then one copy launch unpacking the received buffers into the
+//                ghost planes — a field's g planes are contiguous in the [field][z][y][x]
+//                layout), then the interior launch concurrent with it; the compute stream
+//                waits for the exchange only before the next stage.  Y x Z grid: the four
+//                border boxes (the two z boxes mirrored), then the two-phase exchange (z
+//                planes packed as above, then y rows over the ghost-inclusive z extent —
+//                which also fills the edge ghosts — packed into the staging buffer), then
+//                the interior box.  One rank without ghosts: one launch.
 //   1 out of place  a stage that reads (through a stencil) a field it writes: launch into
 //                the scratch snapshot, copy the saved fields back, exchange (the reference
 //                runs it in place, an order-dependent race; tools/race_check.py).
@@ -31,19 +33,23 @@
 // device zonal table (services series); after each step every sampler records a row.
 //
 // The halo plan (which bytes go to / come from which rank) is built once per action on
-// the host (tclb_amd/parallel/native.py) as lists of HaloOp and PackOp.  Sends and
-// receives between a pair of ranks are matched in issue order (NCCL semantics; tags are
-// for transports that match by tag), which the plan keeps identical on every rank:
-// [sends of fields read from below, to next] [sends of fields read from above, to prev]
-// [receives from prev] [receives from next], fields ascending
-// (tests/test_distributed.py test_native_plan_pairs_by_issue_order).
+// the host (tclb_amd/parallel/native.py) as lists of HaloOp, SegOp, MirrorSpec and PackOp.
+// Sends and receives between a pair of ranks are matched in issue order (NCCL semantics;
+// tags are for transports that match by tag), which the plan keeps identical on every
+// rank: [send up (fields read from below), to next] [send down (fields read from above),
+// to prev] [receive from prev] [receive from next]
+// (tests/test_distributed.py test_native_plan_pairs_by_issue_order).  The IPC transport
+// has no messages: each rank pulls its neighbours' send buffers (SegOp dir 2 / 3) between
+// counter waits (csrc/device/dist.hip xstart_ipc).
 //
 // The services object S supplies the device side (csrc/device/dist.hip GPU, csrc/runtime/
 // dist_cpu.cpp OpenMP):
 //   int run(Launch&)                               one stage launch (the model library)
 //   int sample(Launch&, const SamplePlan&)         one sampler row
 //   int copy_runs(void* dst, const void* src, const LoopPlan&, const StagePlan&)
-//   int xstart(char* snap, const LoopPlan&, const StagePlan&)   start the exchange
+//   int xstart(char* snap, const LoopPlan&, const StagePlan&, int mirrored)   start the
+//                                                  exchange (mirrored: the send buffers
+//                                                  are already filled by the borders)
 //   int xfinish()                                  later launches wait for it
 //   int series(const LoopPlan&, int iter)          active series entries -> zonal table
 //   int part_pre(Launch&, const LoopPlan&), part_post(Launch&, const LoopPlan&, int step)

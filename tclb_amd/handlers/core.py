@@ -245,13 +245,25 @@ class VTK(Callback):
         return self.solver.write_vtk(self.name, self.what, self.reg)
 
 
+def _bool(v) -> bool:
+    """pugixml as_bool: true for a value starting with 1, t, T, y or Y"""
+    return str(v).strip()[:1] in ("1", "t", "T", "y", "Y")
+
+
 @register("HDF5")
 class HDF5(Callback):
     """reference cbHDF5 (src/Handlers/cbHDF5.cpp): region-cropped field output, one HDF5
     file per step (written by the native writer csrc/runtime/h5.cpp, no libhdf5) with an
-    XDMF sidecar (``write_xdmf``).  Datasets are stored contiguous: ``compress`` (deflate)
-    and ``chunk`` are accepted and ignored with a notice, as is ``point_data``;
-    ``format="binary"`` writes a raw binary file plus .xmf instead."""
+    XDMF sidecar (``write_xdmf``).  As the reference: chunked datasets whose chunk dims are
+    negotiated at start as the GCD of every rank's local extent along z, y and x (a chunk
+    never spans two ranks; cbHDF5.cpp:98-126), deflated at level 6 unless
+    ``compress="false"`` (cbHDF5.cpp:20-24); ``point_data`` writes node-centred XDMF;
+    an explicit ``chunk`` is refused, as the reference refuses it.  Deviation: a chunk is
+    capped at 16 MiB by splitting its z (then y) extent along divisors of the negotiated
+    one, so chunks stay under the format's 4 GiB chunk-size field and compress in
+    parallel.  ``format="binary"`` writes a raw binary file plus .xmf instead."""
+
+    CHUNK_CAP = 16 << 20
 
     def init(self):
         super().init()
@@ -265,16 +277,45 @@ class HDF5(Callback):
         self.double = calc_double if prec is None else prec == "double"
         if prec not in (None, "double", "float"):
             raise HandlerError("HDF5 precision should be double or float")
-        for a in ("compress", "chunk", "point_data"):
-            if self.node.get(a) is not None:
-                log.notice(f"HDF5: attribute {a} has no effect (contiguous datasets)")
+        self.deflate = _bool(self.node.get("compress", "true"))
+        self.point_data = _bool(self.node.get("point_data", "false"))
+        if self.node.get("chunk") is not None:
+            raise HandlerError("HDF5: supplying chunk size is not yet supported (as in the reference)")
+        if self.double != calc_double and self.deflate:
+            log.notice("HDF5: writing a different type than the one calculated")
         self.hdf5 = self.node.get("format", "hdf5").lower() != "binary"
         self.xdmf = self.node.get("write_xdmf", "true").lower() in ("true", "1", "yes")
+        self.chunk = self._negotiate_chunks() if self.hdf5 else None
         return 0
+
+    def _negotiate_chunks(self):
+        """GCD over the ranks of the local output extents (z, y, x); ranks without a part
+        of the region take no part (reference cbHDF5::Init)"""
+        import math
+        sv = self.solver
+        lat = sv.lattice
+        X0, Y0, Z0, NX, NY, NZ = self.reg
+        x0, y0, z0 = lat.slab.offset
+        nx, ny, nz = lat.shape
+        ext = (min(z0 + nz, Z0 + NZ) - max(z0, Z0), min(y0 + ny, Y0 + NY) - max(y0, Y0),
+               min(x0 + nx, X0 + NX) - max(x0, X0))
+        mine = ext if min(ext) > 0 else None
+        every = [e for e in sv.comm.gather_objects(mine) if e is not None]
+        cz, cy, cx = (math.gcd(*[e[k] for e in every]) for k in range(3))
+        # cap: the largest divisors of the z (then y) extent keeping a double-vector chunk
+        # within CHUNK_CAP
+        per = 8 * 3
+        while cz > 1 and cz * cy * cx * per > self.CHUNK_CAP:
+            cz = max(d for d in range(1, cz) if cz % d == 0)
+        while cy > 1 and cz * cy * cx * per > self.CHUNK_CAP:
+            cy = max(d for d in range(1, cy) if cy % d == 0)
+        log.output(f"Negotiated HDF5 chunks: {cz}x{cy}x{cx}[x3]")
+        return (cz, cy, cx)
 
     def do_it(self):
         return self.solver.write_xdmf(self.name, self.what, self.reg, double=self.double, hdf5=self.hdf5,
-                                      write_xdmf=self.xdmf)
+                                      write_xdmf=self.xdmf, chunk=self.chunk, deflate=self.deflate,
+                                      point_data=self.point_data)
 
 
 @register("Catalyst")

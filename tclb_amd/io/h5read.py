@@ -3,7 +3,8 @@ read back the contiguous datasets of the HDF5 output (csrc/runtime/h5.cpp) in te
 tools.  It walks the structures the HDF5 file-format specification defines — superblock
 version 0, the root group's symbol-table entry (v1 B-tree of group nodes + local heap of
 names), symbol-table nodes, version-1 object headers with the dataspace (v1), datatype
-(fixed/float), and data-layout (v3 contiguous) messages — and rejects anything else.
+(fixed/float), filter-pipeline (v1, deflate only) and data-layout (v3 contiguous or chunked,
+with the v1 B-tree chunk index) messages — and rejects anything else.
 
     from tclb_amd.io.h5read import read_h5
     data = read_h5("out_HDF5_00000100.h5")     # {name: numpy array}
@@ -64,7 +65,8 @@ def _dataset(b: bytes, oh: int, so: int, sl: int) -> np.ndarray:
         raise H5FormatError("only version-1 object headers are read")
     nmsg, size = _u(b, oh + 2, 2), _u(b, oh + 8, 4)
     p, end = oh + 16, oh + 16 + size
-    shape = dtype = layout = None
+    shape = dtype = layout = chunked = None
+    filters: List[int] = []
     for _ in range(nmsg):
         if p >= end:
             break
@@ -86,11 +88,27 @@ def _dataset(b: bytes, oh: int, so: int, sl: int) -> np.ndarray:
                 dtype = np.dtype("<f" + str(size_b))
             else:
                 raise H5FormatError(f"datatype class {cls}")
+        elif mtype == 0xB:                         # filter pipeline
+            if b[body] != 1:
+                raise H5FormatError("filter pipeline version")
+            q = body + 8
+            for _ in range(b[body + 1]):
+                fid, nlen, _flags, nval = (_u(b, q + 2 * k, 2) for k in range(4))
+                if fid != 1:
+                    raise H5FormatError(f"filter {fid} (only deflate is read)")
+                q += 8 + ((nlen + 7) // 8) * 8 + 4 * nval + (4 if nval % 2 else 0)
+                filters.append(fid)
         elif mtype == 0x8:                         # data layout
-            if b[body] != 3 or b[body + 1] != 1:
-                raise H5FormatError("only contiguous layout v3")
-            layout = (_u(b, body + 2, so), _u(b, body + 2 + so, sl))
+            if b[body] != 3 or b[body + 1] not in (1, 2):
+                raise H5FormatError("only contiguous or chunked layout v3")
+            if b[body + 1] == 1:
+                layout = (_u(b, body + 2, so), _u(b, body + 2 + so, sl))
+            else:
+                nd = b[body + 2]
+                chunked = (_u(b, body + 3, so), [_u(b, body + 3 + so + 4 * k, 4) for k in range(nd)])
         p = body + msize
+    if chunked is not None and shape is not None and dtype is not None:
+        return _chunked(b, shape, dtype, chunked[0], chunked[1], bool(filters), so)
     if shape is None or dtype is None or layout is None:
         raise H5FormatError("dataset without dataspace/datatype/layout")
     addr, nbytes = layout
@@ -98,6 +116,40 @@ def _dataset(b: bytes, oh: int, so: int, sl: int) -> np.ndarray:
     if n * dtype.itemsize != nbytes:
         raise H5FormatError("layout size does not match the dataspace")
     return np.frombuffer(b, dtype=dtype, count=n, offset=addr).reshape(shape).copy()
+
+
+def _chunked(b: bytes, shape, dtype, btree: int, cdims, deflate: bool, so: int) -> np.ndarray:
+    """a chunked dataset: walk the raw-data-chunk B-tree (node type 1), inflate every
+    chunk and place it at its element offsets (edge chunks cropped)"""
+    import zlib
+    rank = len(shape)
+    out = np.zeros(shape, dtype=dtype)
+    cd = cdims[:rank]
+    keysz = 8 + 8 * (rank + 1)
+
+    def node(addr):
+        if b[addr:addr + 4] != b"TREE":
+            raise H5FormatError("bad chunk B-tree signature")
+        if b[addr + 4] != 1:
+            raise H5FormatError("not a raw-data chunk B-tree")
+        level, used = b[addr + 5], _u(b, addr + 6, 2)
+        p = addr + 8 + 2 * so
+        for i in range(used):
+            k = p + i * (keysz + so)
+            size = _u(b, k, 4)
+            off = [_u(b, k + 8 + 8 * d, 8) for d in range(rank)]
+            child = _u(b, k + keysz, so)
+            if level > 0:
+                node(child)
+                continue
+            raw = b[child:child + size]
+            if deflate:
+                raw = zlib.decompress(raw)
+            blk = np.frombuffer(raw, dtype=dtype).reshape(cd)
+            sl = tuple(slice(o, min(o + c, n)) for o, c, n in zip(off, cd, shape))
+            out[sl] = blk[tuple(slice(0, s.stop - s.start) for s in sl)]
+    node(btree)
+    return out
 
 
 def read_h5(path: str) -> Dict[str, np.ndarray]:

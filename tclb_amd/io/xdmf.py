@@ -54,13 +54,18 @@ def write_piece(path: str, region, lreg, fields, lay):
         os.close(fd)
 
 
-def write_xmf(path: str, binname: str, region, lay, spacing: float = 1.0, time: float = 0.0, hdf5: bool = False):
+def write_xmf(path: str, binname: str, region, lay, spacing: float = 1.0, time: float = 0.0, hdf5: bool = False,
+              point_data: bool = False):
     """XDMF sidecar; hdf5=True: the DataItems point into an HDF5 file ("file.h5:/Name", as
-    the reference's hdf5WriteLattice), else into the raw binary file at byte offsets"""
+    the reference's hdf5WriteLattice), else into the raw binary file at byte offsets.
+    point_data: the values sit on the mesh points (a mesh of nz x ny x nx points,
+    Center="Node"), else on the cells of an (nz+1) x (ny+1) x (nx+1) point mesh
+    (reference HDF5_WRITE_POINT, src/hdf5Lattice.cpp:136-141)"""
     X0, Y0, Z0, nx, ny, nz = region
+    pd = 0 if point_data else 1
     lines = ['<?xml version="1.0" ?>', '<!DOCTYPE Xdmf SYSTEM "Xdmf.dtd" []>', '<Xdmf Version="2.0">', '<Domain>',
              '<Grid Name="lattice" GridType="Uniform">', f'<Time Value="{time:g}"/>',
-             f'<Topology TopologyType="3DCoRectMesh" Dimensions="{nz + 1} {ny + 1} {nx + 1}"/>',
+             f'<Topology TopologyType="3DCoRectMesh" Dimensions="{nz + pd} {ny + pd} {nx + pd}"/>',
              '<Geometry GeometryType="ORIGIN_DXDYDZ">',
              f'<DataItem Dimensions="3" NumberType="Float" Format="XML">{Z0 * spacing:g} {Y0 * spacing:g} {X0 * spacing:g}</DataItem>',
              f'<DataItem Dimensions="3" NumberType="Float" Format="XML">{spacing:g} {spacing:g} {spacing:g}</DataItem>',
@@ -74,7 +79,8 @@ def write_xmf(path: str, binname: str, region, lay, spacing: float = 1.0, time: 
         else:
             item = (f'<DataItem Dimensions="{dims}" NumberType="{_XT[dt.kind]}" Precision="{dt.itemsize}" '
                     f'Endian="Little" Format="Binary" Seek="{off}">{binname}</DataItem>')
-        lines += [f'<Attribute Name="{name}" AttributeType="{at}" Center="Cell">', item, '</Attribute>']
+        center = "Node" if point_data else "Cell"
+        lines += [f'<Attribute Name="{name}" AttributeType="{at}" Center="{center}">', item, '</Attribute>']
     lines += ['</Grid>', '</Domain>', '</Xdmf>']
     with open(path, "w") as f:
         f.write("\n".join(lines) + "\n")

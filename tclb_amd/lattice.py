@@ -133,6 +133,8 @@ class Lattice:
         # executor's class tile lists of split stages, Launch.flags_gen)
         self.flags_version = next(_FLAGS_GEN)
         self._kept_cache: Dict[str, List[int]] = {}
+        self._fields_gen = 0              # bumped by set_fields_interior (setting-derived kept fields)
+        self._fill_state = None
         self._iterating = False
         # settings
         self.gsettings = [s.name for s in m.global_settings]
@@ -809,8 +811,28 @@ class Lattice:
         if not idx:
             return
         src, dst = self.snaps[self.cur], self.snaps[1 - self.cur]
+        m = self.model
+        sf = m.setting_fields
+        fill = {}
         for i in idx:
-            dst[i].copy_(src[i])
+            f = m.fields[i]
+            key = f.nicename if f.nicename in sf else (f.name if f.name in sf else None)
+            if key is not None:
+                v = sf[key]
+                fill[i] = float(self.svals[self.gsettings.index(v)]) if isinstance(v, str) else float(v)
+        # setting-derived fields: filled on both snapshots (ghosts included) when their
+        # values or the fields changed since the last fill — what the reference's Run
+        # stores on every node in every step
+        state = (tuple(sorted(fill.items())), self._fields_gen, self.snaps[0].data_ptr(), self.snaps[1].data_ptr())
+        for i in idx:
+            if i in fill:
+                if state != self._fill_state:
+                    sh = float(self._shift_t[i].reshape(-1)[0]) if self._shift_t is not None else 0.0
+                    src[i].fill_(fill[i] - sh)
+                    dst[i].fill_(fill[i] - sh)
+            else:
+                dst[i].copy_(src[i])
+        self._fill_state = state
 
     # ------------------------------------------------------------------ settings
     def set_setting(self, name: str, value: float, zone: Optional[str] = None, _init: bool = False):
@@ -973,6 +995,7 @@ class Lattice:
         if self._shift_t is not None:
             data = data.to(torch.float64) - self._shift_t
         self.snaps[self.cur][:, self.gz:self.gz + nz, self.gy:self.gy + ny, :nx].copy_(data)
+        self._fields_gen += 1
         self.exchange()
 
     def quantity(self, name: str, scale: float = 1.0) -> torch.Tensor:

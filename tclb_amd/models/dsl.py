@@ -156,6 +156,9 @@ class Model:
         # hand-written reverse-mode node adjoints: stage main -> (predicate, function)
         # member names in the dynamics (see set_reverse)
         self.reverse: Dict[str, tuple] = {}
+        # kept fields whose value is a global setting (or a constant) on every node: the
+        # lattice fills them on both snapshots instead of copying them (setting_fields)
+        self.setting_fields: Dict[str, object] = {}
         self.color: Optional[tuple] = None     # (value, weight) C++ expressions of Color()
         # waves/SIMD floor of the globals-integrating stage kernels (0: compiler's choice);
         # see executor_hip.hpp k_stage_glob

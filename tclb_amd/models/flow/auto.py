@@ -100,6 +100,14 @@ def build(q19: bool = False, part: bool = False, coll: str = "MRT", fmt: bool = 
                     lazy_load=True)
         m.add_action("Iteration", ["BaseIteration", "CalcF"])
         m.add_action("Init", ["BaseInit", "CalcF"])
+    else:
+        # without particles Run only sets the Force fields to the body force (reference
+        # Dynamics.c.Rt Run: fx = ForceX ... sol = 0, densities Dynamics.R:24-27) and
+        # nothing in the step reads them: the iteration neither loads nor stores them
+        # (keep); the lattice fills both snapshots from the settings before the steps of
+        # every iterate call in which they changed (Lattice._mirror_kept)
+        m.add_stage("BaseIteration", "Run", load_densities=["f"], save_fields=["f", "Force"], keep=["Force"])
+        m.setting_fields = {"fx": "ForceX", "fy": "ForceY", "fz": "ForceZ", "sol": 0.0}
     for n in ["EPressure", "EVelocity", "Wall", "WPressure", "WVelocity"]:
         m.add_node_type(n, "BOUNDARY")
     m.add_node_type("MRT", "COLLISION")

@@ -31,6 +31,12 @@ def lib():
             L.tclb_stl_cuts.restype = ctypes.c_longlong
             L.tclb_h5_create.argtypes = [ctypes.c_char_p, i, ctypes.c_char_p, P, P, P, P]
             L.tclb_h5_create.restype = ctypes.c_longlong
+            L.tclb_h5_create_chunked.argtypes = [ctypes.c_char_p, i, ctypes.c_char_p, P, P, P, P, i, P, P, P, P]
+            L.tclb_h5_create_chunked.restype = ctypes.c_longlong
+            L.tclb_h5_chunk_bound.argtypes = [i, i, P, P]
+            L.tclb_h5_chunk_bound.restype = ctypes.c_longlong
+            L.tclb_h5_chunk_pack.argtypes = [P, i, i, P, P, i, P, P]
+            L.tclb_h5_chunk_pack.restype = ctypes.c_longlong
             L.tclb_solid_grid.argtypes = [P, i, i, i, i, i, i, P, ctypes.c_longlong]
             L.tclb_solid_grid.restype = ctypes.c_longlong
             L.tclb_nan_scan_f64.argtypes = [P, ctypes.c_longlong]
@@ -113,6 +119,70 @@ def h5_create(path: str, datasets) -> list:
     if r < 0:
         raise OSError(f"cannot write {path}")
     return [int(v) for v in off[:n]]
+
+
+def _h5_meta(datasets):
+    codes = {np.dtype(np.uint8): 0, np.dtype(np.float32): 1, np.dtype(np.float64): 2}
+    n = len(datasets)
+    names = b"".join(nm.encode() + b"\0" for nm, _, _ in datasets)
+    dt = np.array([codes[np.dtype(t)] for _, t, _ in datasets], dtype=np.int32)
+    rk = np.array([len(s) for _, _, s in datasets], dtype=np.int32)
+    dims = np.zeros((max(1, n), 4), dtype=np.int64)
+    for k, (_, _, s) in enumerate(datasets):
+        dims[k, :len(s)] = s
+    return n, names, dt, rk, dims
+
+
+def h5_chunk_pack(a: np.ndarray, cdims, level: int):
+    """the chunks of one rank's local block `a` (chunk dims `cdims` dividing a.shape,
+    row-major over the chunk grid), deflated (level >= 0, the HDF5 deflate filter's zlib
+    format) or raw: returns (bytes as a uint8 array, per-chunk sizes)"""
+    a = np.ascontiguousarray(a)
+    ld = np.array(a.shape, dtype=np.int64)
+    cd = np.array(cdims, dtype=np.int64)
+    if len(ld) != len(cd) or np.any(ld % cd):
+        raise ValueError(f"chunk dims {tuple(cd)} do not tile {tuple(ld)}")
+    L = lib()
+    bound = L.tclb_h5_chunk_bound(a.itemsize, a.ndim, ld.ctypes.data, cd.ctypes.data)
+    out = np.empty(max(1, bound), dtype=np.uint8)
+    sizes = np.zeros(int(np.prod(ld // cd)), dtype=np.int64)
+    r = L.tclb_h5_chunk_pack(a.ctypes.data, a.itemsize, a.ndim, ld.ctypes.data, cd.ctypes.data, int(level),
+                             out.ctypes.data, sizes.ctypes.data)
+    if r < 0:
+        raise RuntimeError("HDF5 chunk compression failed")
+    return out[:r], sizes
+
+
+def h5_create_chunked(path: str, datasets, cdims, level: int, chunks) -> list:
+    """write the metadata and chunk indexes of an HDF5 file of chunked datasets
+    [(name, dtype, shape)] with chunk dims cdims[i] and deflate `level` (< 0: none);
+    chunks[i] = [(element offsets, stored size)] in the order the chunks are to be placed;
+    returns each dataset's chunk addresses in that order"""
+    n, names, dt, rk, dims = _h5_meta(datasets)
+    cd = np.zeros((max(1, n), 4), dtype=np.int64)
+    for k, c in enumerate(cdims):
+        cd[k, :len(c)] = c
+    nch = np.array([len(c) for c in chunks] or [0], dtype=np.int64)
+    tot = int(nch.sum())
+    coff = np.zeros((max(1, tot), 4), dtype=np.int64)
+    csz = np.zeros(max(1, tot), dtype=np.int64)
+    j = 0
+    for lst in chunks:
+        for off, sz in lst:
+            coff[j, :len(off)] = off
+            csz[j] = sz
+            j += 1
+    addr = np.zeros(max(1, tot), dtype=np.int64)
+    r = lib().tclb_h5_create_chunked(path.encode(), n, names, dt.ctypes.data, rk.ctypes.data, dims.ctypes.data,
+                                     cd.ctypes.data, int(level), nch.ctypes.data, coff.ctypes.data, csz.ctypes.data,
+                                     addr.ctypes.data)
+    if r < 0:
+        raise OSError(f"cannot write {path}")
+    out, j = [], 0
+    for lst in chunks:
+        out.append([int(v) for v in addr[j:j + len(lst)]])
+        j += len(lst)
+    return out
 
 
 def png_write(path: str, rgba: np.ndarray):

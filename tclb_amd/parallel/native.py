@@ -9,14 +9,28 @@ RunInterior -> MPIStream_B (src/Lattice.cu.Rt:466-533,900-989), particle stages 
 CopyInParticles / CopyOutParticles (:392-437), fixed-point stages (:484), the zone index of
 the time series (:473-477), samplers (:1376-1389).
 
-Transports (``TCLB_DIST_TRANSPORT`` = auto | rccl | copy):
+Transports (``TCLB_DIST_TRANSPORT`` = auto | rccl | ipc | copy):
+
+Every stage exchanges ONE packed message per neighbour and direction (phase_a): the border
+launches mirror their stores of the exchanged fields into contiguous send buffers
+(core.hpp mirror_store; pack segments where no border split runs), and one copy launch
+unpacks what arrived into the ghost planes (round 5 sent one message per field: 36 RCCL
+operations per d3q27 stage).
 
 * ``rccl``     — GPU: this module's own RCCL communicator (librccl dlopen'ed from torch's
-  lib dir; the unique id travels through torch.distributed), grouped ncclSend/ncclRecv of
-  each halo field's planes straight from / into the output snapshot on a high-priority
-  comm stream (no pack, no unpack; the Y x Z grid's y rows go through a staging buffer),
-  ncclAllReduce of the particle forces.  With one rank (LoopbackComm) the peer is the rank
-  itself: RCCL self send/receive, so a single MI355X exercises the multi-GPU code.
+  lib dir; the unique id travels through torch.distributed), one grouped ncclSend/ncclRecv
+  per neighbour of the packed buffers on a high-priority comm stream, ncclAllReduce of the
+  particle forces.  With one rank (LoopbackComm) the peer is the rank itself: RCCL self
+  send/receive, so a single MI355X exercises the multi-GPU code.
+* ``ipc``      — GPU, no collective library: every rank's staging buffer and a block of
+  counters live in device memory the other ranks map (hipIpcGetMemHandle / OpenMemHandle,
+  handles through torch.distributed).  A rank publishes READY when its send buffers are
+  written, pulls its neighbours' buffers straight into its ghost planes (one copy kernel,
+  peer reads over xGMI) after their READY, publishes DONE, and waits for the neighbours'
+  DONE before the buffers are rewritten; the particle forces are summed from every rank's
+  shared copy in rank order.  Waits are bounded (TCLB_IPC_TIMEOUT_S).  This is also the
+  transport of several processes on ONE device (a gloo process group), which RCCL refuses:
+  the multi-process path runs on a single MI355X (tests/test_gpu_ipc.py).
 * ``copy``     — one rank as its own neighbour (or no neighbour at all), the plan executed
   as device-to-device copies (GPU) or memcpy (CPU).
 * ``callback`` — CPU ranks (gloo): the loop calls back into Python per exchange phase and

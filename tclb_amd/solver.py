@@ -11,7 +11,7 @@ import json
 import os
 import time
 import xml.etree.ElementTree as ET
-from typing import Dict, List, Optional, Sequence
+from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
 import torch
@@ -271,13 +271,18 @@ class Solver:
         return 0
 
     def write_xdmf(self, name: str, what: Optional[Sequence[str]], region=None, double: bool = True,
-                   hdf5: bool = True, write_xdmf: bool = True):
+                   hdf5: bool = True, write_xdmf: bool = True, chunk: Optional[Tuple[int, int, int]] = None,
+                   deflate: bool = True, point_data: bool = False):
         """HDF5 callback output (reference hdf5WriteLattice + XDMF, src/hdf5Lattice.cpp:26-339):
-        one HDF5 file per step with a contiguous dataset per flag group (uint8) and per
-        selected quantity (vectors (nz, ny, nx, 3)) over the output region, written by the
-        native writer (csrc/runtime/h5.cpp: rank 0 lays out the metadata, every rank
-        pwrite()s its own slab rows into the data blocks), and an XDMF sidecar.  hdf5=False
-        writes the same blocks as one raw binary file instead."""
+        one HDF5 file per step with a dataset per flag group (uint8) and per selected
+        quantity (vectors (nz, ny, nx, 3)) over the output region, written by the native
+        writer (csrc/runtime/h5.cpp), and an XDMF sidecar (point_data: node-centred, as the
+        reference's HDF5_WRITE_POINT).  chunk (z, y, x): chunked datasets, deflated at level
+        6 unless deflate=False (the reference's default) — every rank compresses its own
+        chunks, rank 0 lays out the metadata and chunk indexes from the gathered chunk
+        sizes, every rank writes its chunks at the addresses it is handed.  chunk=None:
+        contiguous datasets, every rank pwrite()s its slab rows.  hdf5=False writes the
+        same blocks as one raw binary file instead."""
         from .io import xdmf
         lat = self.lattice
         fields = self.output_fields(what)
@@ -293,10 +298,12 @@ class Solver:
                 for n, a, nc in fields]
         layout = xdmf.layout(region, meta)
         data = base + (".h5" if hdf5 else ".bin")
-        if hdf5:
+        X0, Y0, Z0, rnx, rny, rnz = region
+        if hdf5 and chunk is not None:
+            self._write_h5_chunked(data, region, sub, meta, chunk, 6 if deflate else -1)
+        elif hdf5:
             # dataset data blocks at the offsets the native writer chose (rank 0)
             from .ops.host import h5_create
-            _, _, _, rnx, rny, rnz = region
             shapes = [(n, dt, (rnz, rny, rnx) + ((nc,) if nc > 1 else ())) for n, dt, nc, _ in layout]
             offs = None
             if self.rank == 0:
@@ -308,16 +315,74 @@ class Solver:
         elif self.rank == 0:
             log.output(f"{self.iter:8d} it writing xdmf {base}.xmf")
             xdmf.create(data, layout)
-        self.comm.barrier()
-        if sub is not None:
-            lreg, lfields = sub
-            xdmf.write_piece(data, region, lreg, [(n, np.asarray(a).astype(t, copy=False), nc)
-                                                for (n, a, nc), (_, t, _) in zip(lfields, meta)], layout)
+        if not (hdf5 and chunk is not None):
+            self.comm.barrier()
+            if sub is not None:
+                lreg, lfields = sub
+                xdmf.write_piece(data, region, lreg, [(n, np.asarray(a).astype(t, copy=False), nc)
+                                                    for (n, a, nc), (_, t, _) in zip(lfields, meta)], layout)
         self.comm.barrier()
         if self.rank == 0 and (write_xdmf or not hdf5):
             xdmf.write_xmf(base + ".xmf", os.path.basename(data), region, layout, spacing,
-                           time=self.iter * self.units.alt("1s") if self.units.alt("1s") else self.iter, hdf5=hdf5)
+                           time=self.iter * self.units.alt("1s") if self.units.alt("1s") else self.iter, hdf5=hdf5,
+                           point_data=point_data)
         return 0
+
+    def _write_h5_chunked(self, data: str, region, sub, meta, chunk, level: int):
+        """chunked (and deflated) HDF5 datasets: each rank packs the chunks of its block,
+        rank 0 writes the metadata from the gathered chunk lists, each rank writes its
+        chunks (one run per dataset) at the addresses rank 0 hands out"""
+        from .ops.host import h5_chunk_pack, h5_create_chunked
+        X0, Y0, Z0, rnx, rny, rnz = region
+        blobs, info = [], None
+        if sub is not None:
+            (x0, y0, z0, _, _, _), lfields = sub
+            info = []
+            for (n, a, nc), (_, t, _) in zip(lfields, meta):
+                a = np.asarray(a)
+                if nc > 1:
+                    a = np.moveaxis(a, 0, -1)                # (nz, ny, nx, nc)
+                a = np.ascontiguousarray(a.astype(np.dtype(t).newbyteorder("<"), copy=False))
+                cd = tuple(chunk) + ((nc,) if nc > 1 else ())
+                blob, sizes = h5_chunk_pack(a, cd, level)
+                grid = [a.shape[k] // cd[k] for k in range(a.ndim)]
+                o0 = (z0 - Z0, y0 - Y0, x0 - X0, 0)
+                offs = [tuple(o0[k] + idx[k] * cd[k] for k in range(a.ndim))
+                        for idx in np.ndindex(*grid)]
+                blobs.append(blob)
+                info.append((offs, [int(v) for v in sizes]))
+        every = self.comm.gather_objects(info)
+        addrs = None
+        if self.rank == 0:
+            log.output(f"{self.iter:8d} it writing hdf5 {data}")
+            os.makedirs(os.path.dirname(data) or ".", exist_ok=True)
+            shapes, cdims, chunks = [], [], []
+            for i, (n, t, nc) in enumerate(meta):
+                shapes.append((n, t, (rnz, rny, rnx) + ((nc,) if nc > 1 else ())))
+                cdims.append(tuple(chunk) + ((nc,) if nc > 1 else ()))
+                chunks.append([(o, s) for r in every if r is not None for o, s in zip(*r[i])])
+            flat = h5_create_chunked(data, shapes, cdims, level, chunks)
+            # the address of each rank's first chunk per dataset (its chunks are one run)
+            addrs, k = [], [0] * len(meta)
+            for r in every:
+                if r is None:
+                    addrs.append(None)
+                    continue
+                row = []
+                for i in range(len(meta)):
+                    row.append(flat[i][k[i]] if r[i][0] else 0)
+                    k[i] += len(r[i][0])
+                addrs.append(row)
+        mine = self.comm.scatter_objects(addrs) if self.comm.size > 1 else addrs[0]
+        self.comm.barrier()
+        if sub is not None:
+            fd = os.open(data, os.O_WRONLY)
+            try:
+                for blob, at in zip(blobs, mine):
+                    if blob.size:
+                        os.pwrite(fd, blob.tobytes(), at)
+            finally:
+                os.close(fd)
 
     def write_txt(self, name: str, what: Optional[Sequence[str]], gzip: bool = False):
         prefix = self.out_iter_file(name, "")

@@ -9,7 +9,12 @@ SMALL_2D = (40, 24, 1)
 SMALL_3D = (24, 12, 10)
 
 
-def collision_value(m):
+def collision_value(m, name=None):
+    """the node type every node is flagged with: the case's "_flag" (a collision type the
+    model's Run() dispatches) or the model's first COLLISION type"""
+    flag = case_settings(name or m.name).get("_flag")
+    if flag and m.node_type(flag) is not None:
+        return m.node_type(flag).value
     for g in ("COLLISION",):
         for n in m.node_types:
             if n.group == g:
@@ -55,6 +60,12 @@ CASE_SETTINGS = {
                                  "T_init": 1.0, "dT": 0.05, "sigma_T": -1e-4, "k_h": 0.05, "k_l": 0.02,
                                  "cp_h": 1.0, "cp_l": 1.0},
     "d3q27_tePSM_per": {"omegaF": 1.0, "FluidConductivity": 0.2, "SolidConductivity": 0.5},
+    # the finite-difference PDEs: their defaults (zero diffusivity, zero velocity) leave a
+    # state unchanged, so a benchmark of them would time a copy
+    "diffusion2D": {"diff_coeff": 0.1},
+    "advection_diffusion2D": {"diff_coeff": 0.1, "ux": 0.05, "uy": 0.02},
+    # Run() has no case for the first COLLISION type (CM): flag the higher-order CM collision
+    "d2q9q9_cm_cht": {"_flag": "CM_HIGHER"},
     "d3q27_pf_velocity": {"Density_h": 1.0, "Density_l": 0.1, "sigma": 1e-3, "Viscosity_l": 0.05,
                           "Viscosity_h": 0.05, "M": 0.05, "PhaseField": 1.0, "Radius": 4.0,
                           "CenterX": 12.0, "CenterY": 6.0, "CenterZ": 5.0, "BubbleType": -1.0},
@@ -75,7 +86,7 @@ def make_case(name, device="cpu", precision="double", shape=None, comm=None, **k
     shape = shape or (SMALL_2D if m.dims == 2 else SMALL_3D)
     lat = Lattice(name, shape, device=torch.device(device), precision=precision, comm=comm, **kw)
     nx = shape[0]
-    fl = np.full((lat.NZ, lat.NY, nx), collision_value(m), dtype=np.uint32)
+    fl = np.full((lat.NZ, lat.NY, nx), collision_value(m, name), dtype=np.uint32)
     wall = m.node_type("Wall")
     if wall is not None and not case_settings(name).get("_no_walls"):
         fl[:, :, 0] = wall.value   # x = 0 plane of walls (not on the decomposed axis)

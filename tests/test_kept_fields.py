@@ -5,6 +5,7 @@ lattice copies them into the other snapshot before an action with such a stage r
 build that still stored them (every field of the current snapshot after an odd number of
 steps, so the mirror is needed for them to be right)."""
 import json
+import sys
 import os
 
 import pytest
@@ -77,3 +78,21 @@ def test_thermo_kept_fields_match_storing_build():
             for k, v in (("sum", float(a[i].sum())), ("l2", float(a[i].pow(2).sum().sqrt()))):
                 r = ref[key][k][i]
                 assert abs(v - r) <= 1e-12 * max(1.0, abs(r)), (key, lat.model.fields[i].name, k, v, r)
+
+
+def test_auto_force_fields_from_settings():
+    """auto (no particles) no longer loads or stores fx, fy, fz, sol in its iteration:
+    they are filled from ForceX/Y/Z on both snapshots (Lattice._mirror_kept).  Fields,
+    quantities and the flux equal the model that stored them every step
+    (tests/data/auto_force_ref.npz), bit for bit, including after a mid-run change of
+    ForceX / ForceZ, in fp64 and in shifted fp32 storage."""
+    import numpy as np
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    import auto_force_case
+    ref = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "data", "auto_force_ref.npz"))
+    for p in ("double", "mixed-shift"):
+        got = auto_force_case.run(p)
+        for k, v in got.items():
+            assert np.array_equal(v, ref[f"{p}_{k}"]), (p, k, float(np.abs(v - ref[f"{p}_{k}"]).max()))
+    st = Lattice("auto_d3q19_BGK", (4, 4, 4)).model.stage("BaseIteration")
+    assert st.keep == ["Force"] and "Force" not in (st.save_fields or [])

@@ -45,7 +45,7 @@ def main():
     ap.add_argument("--models", default="")
     ap.add_argument("--n3", type=int, default=256)
     ap.add_argument("--n2", type=int, default=4096)
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=100, help="timed iterations (BASELINE.md: >= 100)")
     ap.add_argument("--precision", default="double")
     ap.add_argument("--variants", default="", help="comma list of HIP build variants to A/B (interleaved)")
     ap.add_argument("--rounds", type=int, default=1)
@@ -74,7 +74,8 @@ def main():
             lat = Lattice(name, shape, device=dev, precision=a.precision, variant=variant)
             if split is not None:
                 lat.set_tile_split(split)
-            coll = m.node_type(a.flag).value if a.flag else collision_flag(m)
+            cf = case_settings(name).get("_flag")
+            coll = m.node_type(a.flag).value if a.flag else (m.node_type(cf).value if cf else collision_flag(m))
             lat.set_flags(np.full((lat.NZ, lat.NY, shape[0]), coll, dtype=np.uint32))
             # the model-family settings of the catalog tests (a physical case; some
             # defaults, e.g. zero densities of the phase-field models, are not)
@@ -82,14 +83,20 @@ def main():
                 if not k.startswith("_") and m.setting(k) is not None:
                     lat.set_setting(k, v)
             lat.init()
-            lat.iterate(3, glob_last=False)
+
+            def window():
+                if a.glob_every_step:
+                    for _ in range(a.steps):
+                        lat.iterate(1, glob_last=True, reduce=False)
+                else:
+                    lat.iterate(a.steps, glob_last=True)
+            # warm-up: the exact timed sequence once (every instantiation the window
+            # launches — the globals step included — has run before the clock starts;
+            # round 5 timed advection_diffusion2D's first globals launch, 2.34 ms)
+            window()
             sync()
             t = time.perf_counter()
-            if a.glob_every_step:
-                for _ in range(a.steps):
-                    lat.iterate(1, glob_last=True, reduce=False)
-            else:
-                lat.iterate(a.steps, glob_last=True)
+            window()
             sync()
             dt = (time.perf_counter() - t) / a.steps
             ok = state_finite(lat)
