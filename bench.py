@@ -212,7 +212,7 @@ def main():
         bytes_node = 2 * nf * es + (2 if lat.model.flag_bits == 16 else 4)
         out = {
             "metric": METRIC,
-            "value": round(mlups, 2),
+            "value": float(f"{mlups:.8g}"),
             "unit": "MLUPS",
             "n_gpus": world,
             "steps": a.steps,

@@ -3,7 +3,7 @@
 # headline (512x512x64 fp64) and the 4-GPU part256 case (256x256x64) stepped as one rank
 # through the multi-rank loop with each transport (copy / RCCL to itself / IPC pull from
 # itself), against the plain one-rank lattice; kernel traces of the RCCL and IPC steps.
-#   TAG=r06a scripts/halo_ab.sh [tests] [ab] [prof]
+#   TAG=r06a scripts/halo_ab.sh [tests] [ab] [prof] [models2d] [cavity] [catalog] [headline]
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}; TAG=${TAG:-halo}; O=$R/gpurun_out/$TAG; mkdir -p $O; cd $R
 step() { local name=$1 t=$2 log=$3; shift 3; echo "== $name"; timeout -k 10 $t "$@" > $log 2>&1; local rc=$?; tail -3 $log; echo "   rc=$rc"; if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi; return 0; }
@@ -27,4 +27,14 @@ prof)
     step "rocprof slab $t" 400 $O/prof_slab_$t.log rocprofv3 --kernel-trace --stats -d $O/prof_slab_$t -o run --output-format csv -- python3 $R/bench.py --shape 512,512,64 --steps 20 --warmup 2 --loopback-dist --transport $t
     step "rocprof part slab $t" 400 $O/prof_part_$t.log rocprofv3 --kernel-trace --stats -d $O/prof_part_$t -o run --output-format csv -- python3 $R/tools/bench_configs.py --configs part256 --shape 256,256,64 --steps 20 --warmup 2 --loopback-dist --transport $t
   done ;;
+models2d)
+  step "2-D multi-stage models fp64" 600 $O/models2d.jsonl python tools/perf_models.py --models d2q9_pf_velocity,d2q9_csf,d2q9_lee --n2 2048 --steps 100 --allow-invalid
+  step "rocprof 2-D models" 400 $O/prof_models2d.log rocprofv3 --kernel-trace --stats -d $O/prof_models2d -o run --output-format csv -- python3 $R/tools/perf_models.py --models d2q9_pf_velocity,d2q9_csf --n2 2048 --steps 20 --allow-invalid ;;
+cavity)
+  step "cavity fp64" 300 $O/cavity_fp64.jsonl python tools/bench_configs.py --configs cavity --steps 100 --warmup 10
+  step "cavity ms" 300 $O/cavity_ms.jsonl python tools/bench_configs.py --configs cavity --steps 100 --warmup 10 --precision mixed-shift ;;
+catalog)
+  step "catalog fp64" 1100 $O/catalog_perf.jsonl python tools/perf_models.py --n3 256 --n2 2048 --steps 100 --allow-invalid ;;
+headline)
+  step "bench fp64" 300 $O/bench_fp64.json python bench.py ;;
 esac; done

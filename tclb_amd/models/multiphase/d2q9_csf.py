@@ -56,7 +56,10 @@ def build(bc=False, bcinit=False, noflow=False, weno=False, viscstep=False, cumu
     m.add_field("nw_x", stencil2d=1, group="nw")
     m.add_field("nw_y", stencil2d=1, group="nw")
     m.add_field("phi", stencil2d=1)
-    m.add_stage("BaseIteration", "Run", load_densities=["f", "h", "HZ", "BC"], save_fields=["f", "h", "nw", "HZ"])
+    # keep: the wall normals are set by the fixed-point CalcWallNormall of Init only; Run
+    # reads them and stores them back unchanged (the reference stores them every step)
+    m.add_stage("BaseIteration", "Run", load_densities=["f", "h", "HZ", "BC"], save_fields=["f", "h", "nw", "HZ"],
+                keep=["nw"])
     m.add_stage("CalcPhi", "CalcPhi", save_fields=["phi"], load_densities=["h"])
     m.add_stage("BaseInit", "Init", load_densities=["BC"], save_fields=["f", "h", "HZ"])
     m.add_stage("CalcWallNormall", "CalcNormal", save_fields=["nw"], fixed_point=True)

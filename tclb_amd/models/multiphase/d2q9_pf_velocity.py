@@ -60,9 +60,20 @@ def build(gf=False, rt=False, outflow=False, debug=False, bgk=False, cm=False, g
         m.add_stage("PhaseInit", "Init_phase", save_fields=["PF"])
         m.add_stage("WallInit", "Init_wallNorm", save_fields=["nw"])
         m.add_stage("BaseInit", "Init_distributions", save_fields=["g", "h", "Vel"])
-        m.add_stage("BaseIter", "calcHydroIter", save_fields=sv, load_densities=sv)
-        m.add_stage("PhaseIter", "calcPhaseFIter", save_fields=["PF"], load_densities=sv)
-        m.add_stage("WallIter", "calcWallPhaseIter", save_fields=["PF"], load_densities=["nw"])
+        # keep: the wall normals are written by WallInit only (the reference stores them
+        # again in every iteration)
+        m.add_stage("BaseIter", "calcHydroIter", save_fields=sv, load_densities=sv, keep=["nw"])
+        # lazy: a node without a boundary condition sums its pulled h populations and
+        # reads nothing else (PF2_LAZY in the node code); boundary nodes pull every
+        # declared density for BC_Switcher, as before
+        m.add_stage("PhaseIter", "calcPhaseFIter", save_fields=["PF"], load_densities=sv, lazy_load=True)
+        # split: on the GPU only the wall nodes run (node_class_ 2); every other node would
+        # store the PhaseF it reads, in place (the stage is never an action's first)
+        m.add_stage("WallIter", "calcWallPhaseIter", save_fields=["PF"], load_densities=["nw"], split=True)
+        m.defines["PF2_LAZY"] = "1"
+        m.add_codegen(lambda _m: "\n".join(f"  static constexpr int FI_{a.upper()}0 = "
+                                           f"{[i for i, f in enumerate(_m.fields) if f.array == a][0]};"
+                                           for a in ("h",)))
     m.add_action("Iteration", ["BaseIter", "PhaseIter", "WallIter"])
     m.add_action("Init", ["PhaseInit", "WallInit", "WallIter", "BaseInit"])
     m.add_quantity("Rho", unit="kg/m3")

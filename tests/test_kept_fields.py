@@ -96,3 +96,32 @@ def test_auto_force_fields_from_settings():
             assert np.array_equal(v, ref[f"{p}_{k}"]), (p, k, float(np.abs(v - ref[f"{p}_{k}"]).max()))
     st = Lattice("auto_d3q19_BGK", (4, 4, 4)).model.stage("BaseIteration")
     assert st.keep == ["Force"] and "Force" not in (st.save_fields or [])
+
+
+def test_d2q9_pf_velocity_lazy_split_unchanged():
+    """d2q9_pf_velocity (default build) keeps its wall normals, pulls only h in PhaseIter
+    on nodes without a boundary condition and runs WallIter on wall nodes only (split, GPU):
+    fields, globals and the phase-field quantity equal the model that did none of it
+    (tests/data/pf2_ref.npz), bit for bit"""
+    import numpy as np
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    import pf2_case
+    ref = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "data", "pf2_ref.npz"))
+    got = pf2_case.run()
+    for k, v in got.items():
+        assert np.array_equal(v, ref[k]), (k, float(np.abs(v - ref[k]).max()))
+    m = Lattice("d2q9_pf_velocity", (8, 8, 1)).model
+    assert m.stage("BaseIter").keep == ["nw"] and m.stage("PhaseIter").lazy_load and m.stage("WallIter").split
+
+
+def test_d2q9_csf_keeps_wall_normals():
+    """d2q9_csf's iteration keeps (no longer stores) the wall normals: fields, the
+    WallNormal quantity and globals equal the model that stored them (tests/data/
+    csf_ref.npz), bit for bit, on a drop touching a wall"""
+    import numpy as np
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    import csf_case
+    ref = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "data", "csf_ref.npz"))
+    for k, v in csf_case.run().items():
+        assert np.array_equal(v, ref[k]), (k, float(np.abs(v - ref[k]).max()))
+    assert Lattice("d2q9_csf", (8, 8, 1)).model.stage("BaseIteration").keep == ["nw"]

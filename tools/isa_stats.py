@@ -12,6 +12,7 @@ they are the budget a change to the node code is weighed by (round-4 counters: t
 pf_velocity mixed-shift collide issued 1 433 VALU per wave).
 
     python tools/isa_stats.py d3q27_pf_velocity [--variant V] [--match 'k_stage<'] [--stage 0]
+    python tools/isa_stats.py --scan [--min-regs 256]    # every model: kernels above 256 regs
 """
 from __future__ import annotations
 
@@ -109,7 +110,42 @@ def demangle(names):
     return r.stdout.splitlines()
 
 
+def scan(min_regs: int, match: str):
+    """every built model library (default variants): the kernels whose unified register
+    count (arch VGPRs + AGPRs) exceeds min_regs — the ones whose occupancy and register
+    allocation (AGPR use, spills) make them the riskiest code the compiler emits here"""
+    from tclb_amd import build as B
+    from tclb_amd.models import registry
+    print("model,kernel,vgpr,agpr,scratch,waves_per_simd")
+    for name in registry.all_variants():
+        so = B.lib_path(name, "hip", "")
+        if not os.path.exists(so):
+            continue
+        with tempfile.TemporaryDirectory() as tmp:
+            try:
+                meta = kernels(code_object(so, tmp))
+            except (subprocess.CalledProcessError, IndexError):
+                continue
+        big = [n for n in sorted(meta) if meta[n]["vgpr"] > min_regs]
+        for n, d in zip(big, demangle(big)):
+            if match not in d:
+                continue
+            mt = meta[n]
+            waves = min(8, 512 // ((mt["vgpr"] + 7) // 8 * 8))
+            short = re.sub(r"tclb::M_\w+::Model, ", "", d)
+            short = short if len(short) < 120 else short[:117] + "..."
+            print(f"{name},\"{short}\",{mt['vgpr']},{mt['agpr']},{mt['scratch']},{waves}", flush=True)
+
+
 def main():
+    if "--scan" in sys.argv:
+        ap = argparse.ArgumentParser()
+        ap.add_argument("--scan", action="store_true")
+        ap.add_argument("--min-regs", type=int, default=256)
+        ap.add_argument("--match", default="tclb::exec::k_")
+        a = ap.parse_args()
+        scan(a.min_regs, a.match)
+        return
     ap = argparse.ArgumentParser()
     ap.add_argument("model")
     ap.add_argument("--variant", default="")
