@@ -3,12 +3,14 @@
 # headline (512x512x64 fp64) and the 4-GPU part256 case (256x256x64) stepped as one rank
 # through the multi-rank loop with each transport (copy / RCCL to itself / IPC pull from
 # itself), against the plain one-rank lattice; kernel traces of the RCCL and IPC steps.
-#   TAG=r06a scripts/halo_ab.sh [tests] [ab] [prof] [models2d] [cavity] [catalog] [headline]
+#   TAG=r06a scripts/halo_ab.sh [alltests] [tests] [ab] [prof] [models2d] [cavity] [catalog] [headline]
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}; TAG=${TAG:-halo}; O=$R/gpurun_out/$TAG; mkdir -p $O; cd $R
 step() { local name=$1 t=$2 log=$3; shift 3; echo "== $name"; timeout -k 10 $t "$@" > $log 2>&1; local rc=$?; tail -3 $log; echo "   rc=$rc"; if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi; return 0; }
 export TMPDIR=/tmp
 for W in "$@"; do case $W in
+alltests)
+  step "gpu tests" 900 $O/pytest_gpu.log python -u -m pytest tests -v -m gpu --timeout 300 --timeout-method thread ;;
 tests)
   step "ipc + production tests" 600 $O/pytest_ipc.log python -u -m pytest tests/test_gpu_ipc.py tests/test_gpu_production.py -v -m gpu --timeout 300 --timeout-method thread ;;
 ab)

@@ -399,6 +399,12 @@ struct GpuSvc {
     return hip_check(hipEventRecord(c->done, c->cs), "hipEventRecord");
   }
   int xfinish() { return hip_check(hipStreamWaitEvent(ks, c->done, 0), "hipStreamWaitEvent"); }
+  // the comm stream after the work on ks (the border launches of overlap 2 go there)
+  void* fork() {
+    (void)hipEventRecord(c->ready, ks);
+    (void)hipStreamWaitEvent(c->cs, c->ready, 0);
+    return (void*)c->cs;
+  }
 
   int series(const tclb::LoopPlan& P, int iter) {
     k_series<<<(P.nseries + 63) / 64, 64, 0, ks>>>(P.zonal, P.series, P.nseries, P.svals, P.sslopes, iter);

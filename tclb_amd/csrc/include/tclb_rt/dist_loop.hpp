@@ -51,6 +51,8 @@
 //                                                  exchange (mirrored: the send buffers
 //                                                  are already filled by the borders)
 //   int xfinish()                                  later launches wait for it
+//   void* fork()                                   the comm stream, ordered after the work
+//                                                  queued so far (overlap 2 borders)
 //   int series(const LoopPlan&, int iter)          active series entries -> zonal table
 //   int part_pre(Launch&, const LoopPlan&), part_post(Launch&, const LoopPlan&, int step)
 #pragma once
@@ -152,7 +154,8 @@ struct LoopPlan {
   int axis;         // 0 one rank without ghosts, 1 y slab, 2 z slab, 3 Y x Z grid
   int n, g;         // slab: interior extent and ghost depth along the split axis
   int ny, nz, gy, gz;  // grid: interior extents and ghost depths
-  int overlap;      // border / exchange / interior split
+  int overlap;      // border / exchange / interior split (2: the border launches and the
+                    // exchange on the comm stream, concurrent with the interior launch)
   int nstages;
   StagePlan st[DIST_MAX_STAGES];
   const HaloOp* ops;
@@ -237,6 +240,17 @@ inline int loop_full(S& sv, Launch& L, const LoopPlan& P, int nx) {
   return sv.run(L);
 }
 
+// the border launches of a stage: on the compute stream before the interior (overlap 1),
+// or on the comm stream (overlap 2) — forked after the work already queued, so they, the
+// exchange that follows them and the interior launch run concurrently; the next stage
+// waits for both (xfinish).  Returns the stream the interior launch goes to.
+template <class S>
+inline void* loop_borders_begin(S& sv, Launch& L, const LoopPlan& P) {
+  void* ks = L.stream;
+  if (P.overlap == 2) L.stream = sv.fork();
+  return ks;
+}
+
 // launch + exchange of one stage in place (mode 0)
 template <class S>
 inline int loop_stage_plain(S& sv, Launch& L, const LoopPlan& P, const StagePlan& st, char* out, int nx) {
@@ -248,10 +262,12 @@ inline int loop_stage_plain(S& sv, Launch& L, const LoopPlan& P, const StagePlan
     if (P.overlap && ny > 2 * gy && nz > 2 * gz) {
       const int box[4][4] = {{0, ny, 0, gz}, {0, ny, nz - gz, nz}, {0, gy, gz, nz - gz}, {ny - gy, ny, gz, nz - gz}};
       const int mir[4] = {st.mir_lo, st.mir_hi, -1, -1};
+      void* ks = loop_borders_begin(sv, L, P);
       for (int b = 0; b < 4; b++) {
         L.ylo = box[b][0], L.yhi = box[b][1], L.zlo = box[b][2], L.zhi = box[b][3];
         if ((r = loop_run_mirrored(sv, L, P, mir[b])) != 0) return r;
       }
+      L.stream = ks;
       if ((r = sv.xstart(out, P, st, 1)) != 0) return r;
       L.ylo = gy, L.yhi = ny - gy, L.zlo = gz, L.zhi = nz - gz;
       if ((r = sv.run(L)) != 0) return r;
@@ -263,10 +279,12 @@ inline int loop_stage_plain(S& sv, Launch& L, const LoopPlan& P, const StagePlan
   }
   const int n = P.n, g = P.g, ax = P.axis;
   if (P.overlap && n > 2 * g) {
+    void* ks = loop_borders_begin(sv, L, P);
     loop_set_range(L, ax, 0, g);
     if ((r = loop_run_mirrored(sv, L, P, st.mir_lo)) != 0) return r;
     loop_set_range(L, ax, n - g, n);
     if ((r = loop_run_mirrored(sv, L, P, st.mir_hi)) != 0) return r;
+    L.stream = ks;
     if ((r = sv.xstart(out, P, st, 1)) != 0) return r;
     loop_set_range(L, ax, g, n - g);
     if ((r = sv.run(L)) != 0) return r;

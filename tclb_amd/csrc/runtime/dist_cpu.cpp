@@ -98,6 +98,7 @@ struct CpuSvc {
     return 0;
   }
   int xfinish() { return 0; }
+  void* fork() { return nullptr; }      // one synchronous executor: nothing to fork
 
   int series(const tclb::LoopPlan& P, int iter) {
     for (int i = 0; i < P.nseries; i++) {

@@ -579,7 +579,10 @@ class NativeLoop:
         P = LoopPlan()
         ax = lat.slab.axis if lat.g > 0 else 0
         P.axis = ax
-        P.overlap = 1 if lat.overlap else 0
+        # overlap 2 (GPU): border launches + exchange on the comm stream, concurrent with
+        # the interior launch (TCLB_CONCURRENT_BORDERS=0: before it, on the compute stream)
+        conc = self.gpu and os.environ.get("TCLB_CONCURRENT_BORDERS", "1") != "0"
+        P.overlap = (2 if conc else 1) if lat.overlap else 0
         if ax in (1, 2):
             P.n = lat.shape[2] if ax == 2 else lat.shape[1]
             P.g = lat.g

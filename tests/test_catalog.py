@@ -48,6 +48,7 @@ def test_model_hip_matches_cpu(name):
 DIST_PATHS = {
     "native-rccl": {"TCLB_DIST_NATIVE": "1", "TCLB_DIST_TRANSPORT": "rccl"},
     "native-copy": {"TCLB_DIST_NATIVE": "1", "TCLB_DIST_TRANSPORT": "copy"},
+    "native-ipc": {"TCLB_DIST_NATIVE": "1", "TCLB_DIST_TRANSPORT": "ipc"},
     "py-mirror": {"TCLB_DIST_NATIVE": "0", "TCLB_HALO_MIRROR": "1"},
     "py-pack": {"TCLB_DIST_NATIVE": "0", "TCLB_HALO_MIRROR": "0"},
 }
