@@ -18,10 +18,12 @@ ab)
     step "slab plain" 300 $O/slab_plain_$rep.json python bench.py --shape 512,512,64 --steps 200 --warmup 20
     for t in copy rccl ipc; do
       step "slab $t" 300 $O/slab_${t}_$rep.json python bench.py --shape 512,512,64 --steps 200 --warmup 20 --loopback-dist --transport $t
+      step "slab $t serial borders" 300 $O/slab_${t}_serial_$rep.json env TCLB_CONCURRENT_BORDERS=0 python bench.py --shape 512,512,64 --steps 200 --warmup 20 --loopback-dist --transport $t
     done
     step "part slab plain" 300 $O/part_plain_$rep.jsonl python tools/bench_configs.py --configs part256 --shape 256,256,64 --steps 200 --warmup 20
     for t in copy rccl ipc; do
       step "part slab $t" 300 $O/part_${t}_$rep.jsonl python tools/bench_configs.py --configs part256 --shape 256,256,64 --steps 200 --warmup 20 --loopback-dist --transport $t
+      step "part slab $t serial borders" 300 $O/part_${t}_serial_$rep.jsonl env TCLB_CONCURRENT_BORDERS=0 python tools/bench_configs.py --configs part256 --shape 256,256,64 --steps 200 --warmup 20 --loopback-dist --transport $t
     done
   done ;;
 prof)

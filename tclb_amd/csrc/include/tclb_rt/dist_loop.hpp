@@ -116,6 +116,9 @@ struct StagePlan {
   int npack, nunpack;
   int mir_lo, mir_hi;  // MirrorSpec of the low / high border launch (-1: none)
   int yseg0, nyseg;    // IPC transport: the grid y phase's pulls (dir 3 segments)
+  int mirror;          // 1: the border launches fill the send buffers (no pack segments);
+                       // 0 for split stages, whose class-0 nodes store nothing
+  int reserved;
 };
 
 struct SeriesEntry {
@@ -268,7 +271,7 @@ inline int loop_stage_plain(S& sv, Launch& L, const LoopPlan& P, const StagePlan
         if ((r = loop_run_mirrored(sv, L, P, mir[b])) != 0) return r;
       }
       L.stream = ks;
-      if ((r = sv.xstart(out, P, st, 1)) != 0) return r;
+      if ((r = sv.xstart(out, P, st, st.mirror)) != 0) return r;
       L.ylo = gy, L.yhi = ny - gy, L.zlo = gz, L.zhi = nz - gz;
       if ((r = sv.run(L)) != 0) return r;
       return sv.xfinish();
@@ -285,7 +288,7 @@ inline int loop_stage_plain(S& sv, Launch& L, const LoopPlan& P, const StagePlan
     loop_set_range(L, ax, n - g, n);
     if ((r = loop_run_mirrored(sv, L, P, st.mir_hi)) != 0) return r;
     L.stream = ks;
-    if ((r = sv.xstart(out, P, st, 1)) != 0) return r;
+    if ((r = sv.xstart(out, P, st, st.mirror)) != 0) return r;
     loop_set_range(L, ax, g, n - g);
     if ((r = sv.run(L)) != 0) return r;
     return sv.xfinish();

@@ -631,7 +631,8 @@ class Lattice:
                     self._launch_stage(si, inp, dst, glob)
                     self._halo_finish(self._halo_start(dst, fields))
             elif self.overlap and n > 2 * g:
-                if self.halo_mirror:
+                # a split stage's class-0 nodes store nothing, not even into the mirror
+                if self.halo_mirror and not st.split:
                     hs = self._border_mirrored(si, inp, dst, glob, fields)
                 else:
                     self._launch_stage(si, inp, dst, glob, (0, g))

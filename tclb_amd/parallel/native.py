@@ -82,7 +82,7 @@ class MirrorSpec(ctypes.Structure):
 class StagePlan(ctypes.Structure):
     _fields_ = [(k, ctypes.c_int) for k in ("stage", "mode", "sweeps", "particle", "op0", "nops", "opb0", "nopsb",
                                             "pk0", "npk", "run0", "nruns", "seg0", "npack", "nunpack", "mir_lo",
-                                            "mir_hi", "yseg0", "nyseg")]
+                                            "mir_hi", "yseg0", "nyseg", "mirror", "reserved")]
 
 
 class SeriesEntry(ctypes.Structure):
@@ -541,8 +541,13 @@ class NativeLoop:
             if mode > 0:
                 runs += _runs(fields)
             S.mir_lo = S.mir_hi = -1
+            # a split stage's class-0 nodes store nothing (not even into the mirror): its
+            # send buffers are packed from the snapshot instead
+            S.mirror = 0 if (st.split or field_lists is not None) else 1
             if ax > 0:
                 ops, pks, ups, mirs, nb = self.phase_a(fields, stg_bytes, k, lay, peer_off)
+                if not S.mirror:
+                    mirs = (None, None)
                 stg_bytes += nb
                 S.op0, S.nops = len(allops), len(ops)
                 allops += ops
