@@ -3,7 +3,7 @@
 # headline (512x512x64 fp64) and the 4-GPU part256 case (256x256x64) stepped as one rank
 # through the multi-rank loop with each transport (copy / RCCL to itself / IPC pull from
 # itself), against the plain one-rank lattice; kernel traces of the RCCL and IPC steps.
-#   TAG=r06a scripts/halo_ab.sh [alltests] [tests] [ab] [prof] [models2d] [cavity] [catalog] [headline]
+#   TAG=r06a scripts/halo_ab.sh [alltests] [tests] [ab] [prof] [models2d] [cavity] [catalog] [headline] [cavitycounters] [part]
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}; TAG=${TAG:-halo}; O=$R/gpurun_out/$TAG; mkdir -p $O; cd $R
 step() { local name=$1 t=$2 log=$3; shift 3; echo "== $name"; timeout -k 10 $t "$@" > $log 2>&1; local rc=$?; tail -3 $log; echo "   rc=$rc"; if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi; return 0; }
@@ -41,4 +41,9 @@ catalog)
   step "catalog fp64" 1100 $O/catalog_perf.jsonl python tools/perf_models.py --n3 256 --n2 2048 --steps 100 --allow-invalid ;;
 headline)
   step "bench fp64" 300 $O/bench_fp64.json python bench.py ;;
+cavitycounters)
+  step "counters cavity fp64" 500 $O/counters_cavity.log python tools/counters.py --tag cavity_fp64 --nodes 16777216 --outdir $O/counters -- python3 $R/tools/bench_configs.py --configs cavity --steps 5 --warmup 1 ;;
+part)
+  step "part256 fp64" 300 $O/part256_fp64.jsonl python tools/bench_configs.py --configs part256 --steps 100 --warmup 10
+  step "rocprof part256" 400 $O/prof_part256.log rocprofv3 --kernel-trace --stats -d $O/prof_part256 -o run --output-format csv -- python3 $R/tools/bench_configs.py --configs part256 --steps 20 --warmup 2 ;;
 esac; done

@@ -105,6 +105,7 @@ struct Ctx {
   Comm comm = nullptr;
   hipStream_t cs = nullptr;   // comm stream
   hipEvent_t ready = nullptr, done = nullptr;
+  hipEvent_t fence = nullptr;   // IPC: a system-scope release before READY is published
   // IPC transport
   unsigned long long* sig = nullptr;              // this rank's signal block (exported)
   unsigned long long* hsig[IPC_MAX_RANKS] = {};   // every rank's, mapped (host table)
@@ -226,6 +227,7 @@ __global__ void __launch_bounds__(256) k_nan0(double* a, int n) {
 
 extern "C" int tclb_part_build_grid(const double*, int, int*, int, int, int, int, int, void*, long long, void*);
 extern "C" int tclb_part_build_tree(const double*, int, int*, int, double, void*, long long, void*);
+extern "C" int tclb_part_acc_slots(double*, int, int, void*);
 extern "C" int tclb_part_rigid_step(double*, const double*, const double*, const unsigned char*, int, double, double,
                                     double, int, double, double, double, void*);
 
@@ -364,12 +366,17 @@ struct GpuSvc {
     const unsigned long long mA = peer_mask(P, 0, 1), mB = peer_mask(P, 2, 3);
     const unsigned long long e = ++c->seq[0];
     if (!mirrored && (r = segcopy(base, stg, P, st.seg0, st.npack)) != 0) return r;
+    // the send buffers were written by kernels of this stream (concurrent borders) or of ks:
+    // an event's system-scope release writes every XCD's L2 back before READY goes out, so
+    // a peer GPU reading over xGMI sees them (within one device the kernel boundary would do)
+    if ((r = hip_check(hipEventRecord(c->fence, c->cs), "hipEventRecord")) != 0) return r;
     if ((r = signal(c->cs, SIG_A_READY, e)) != 0 || (r = wait(c->cs, mA, SIG_A_READY, e)) != 0) return r;
     if ((r = segcopy(base, stg, P, st.seg0 + st.npack, st.nunpack)) != 0) return r;
     if ((r = signal(c->cs, SIG_A_DONE, e)) != 0) return r;
     if (st.npk > 0 || st.nyseg > 0) {
       const unsigned long long eb = ++c->seq[1];
       if ((r = packs(base, stg, P.packs + st.pk0, st.npk, 0)) != 0) return r;
+      if ((r = hip_check(hipEventRecord(c->fence, c->cs), "hipEventRecord")) != 0) return r;
       if ((r = signal(c->cs, SIG_B_READY, eb)) != 0 || (r = wait(c->cs, mB, SIG_B_READY, eb)) != 0) return r;
       if ((r = segcopy(base, stg, P, st.yseg0, st.nyseg)) != 0) return r;
       if ((r = packs(base, stg, P.packs + st.pk0, st.npk, 1)) != 0) return r;
@@ -413,7 +420,8 @@ struct GpuSvc {
 
   int part_pre(tclb::Launch& L, const tclb::LoopPlan& P) {
     const tclb::PartPlan& q = *P.part;
-    int r = hip_check(hipMemsetAsync(q.acc, 0, sizeof(double) * 6 * (size_t)(q.n > 0 ? q.n : 1), ks), "memset");
+    const int k = q.nslots > 1 ? q.nslots : 1;
+    int r = hip_check(hipMemsetAsync(q.acc, 0, sizeof(double) * 6 * (size_t)(q.n > 0 ? q.n : 1) * k, ks), "memset");
     if (r != 0) return r;
     if (q.container == 1) r = tclb_part_build_grid(q.P, q.n, q.grid, q.gdim[0], q.gdim[1], q.gdim[2], q.cell, q.ncell,
                                                    q.tmp, q.tmp_bytes, ks);
@@ -424,6 +432,7 @@ struct GpuSvc {
     }
     L.ext[2] = q.P;
     L.ext[3] = q.acc;
+    L.next[3] = k;
     L.next[2] = q.n;
     L.ext[4] = q.container ? q.grid : nullptr;
     L.next[4] = q.container ? q.grid_n : 0;
@@ -434,6 +443,8 @@ struct GpuSvc {
     const tclb::PartPlan& q = *P.part;
     int r;
     const int na = 6 * q.n;
+    if (q.nslots > 1 && na > 0 && (r = tclb_part_acc_slots(q.acc, na, q.nslots, ks)) != 0)
+      return hip_check((hipError_t)r, "accumulator copies");
     if (q.allreduce && c->transport == 1 && c->nranks > 1 && na > 0) {
       // ncclFloat64 = 8, ncclSum = 0; on the compute stream, after the stage's kernels
       if ((r = rccl_check(c, c->R.all_reduce(q.acc, q.acc, (size_t)na, 8, 0, c->comm, ks), "ncclAllReduce")) != 0)
@@ -445,7 +456,8 @@ struct GpuSvc {
       const unsigned long long e = ++c->seq[2];
       const unsigned long long all = c->nranks >= 64 ? ~0ull : ((1ull << c->nranks) - 1);
       if ((r = hip_check(hipMemcpyAsync(q.accbuf, q.acc, sizeof(double) * (size_t)na, hipMemcpyDeviceToDevice, ks),
-                         "hipMemcpyAsync")) != 0)
+                         "hipMemcpyAsync")) != 0 ||
+          (r = hip_check(hipEventRecord(c->fence, ks), "hipEventRecord")) != 0)
         return r;
       if ((r = signal(ks, SIG_R_READY, e)) != 0 || (r = wait(ks, all, SIG_R_READY, e)) != 0) return r;
       k_accsum<<<(na + 255) / 256, 256, 0, ks>>>(q.acc, q.accs, c->nranks, na);
@@ -457,6 +469,7 @@ struct GpuSvc {
       if ((r = hip_check(hipGetLastError(), "k_nan0")) != 0) return r;
     }
     L.next[2] = 0;
+    L.next[3] = 0;
     L.ext[4] = nullptr;
     L.next[4] = 0;
     if (step && q.integrate && q.n > 0) {
@@ -500,7 +513,8 @@ void* tclb_dist_ctx_create(const char* rccl_path, int transport, int nranks, int
   if (hip_check(hipDeviceGetStreamPriorityRange(&lo, &hi), "hipDeviceGetStreamPriorityRange") != 0 ||
       hip_check(hipStreamCreateWithPriority(&c->cs, hipStreamNonBlocking, hi), "hipStreamCreateWithPriority") != 0 ||
       hip_check(hipEventCreateWithFlags(&c->ready, hipEventDisableTiming), "hipEventCreate") != 0 ||
-      hip_check(hipEventCreateWithFlags(&c->done, hipEventDisableTiming), "hipEventCreate") != 0) {
+      hip_check(hipEventCreateWithFlags(&c->done, hipEventDisableTiming), "hipEventCreate") != 0 ||
+      hip_check(hipEventCreateWithFlags(&c->fence, hipEventDisableTiming), "hipEventCreate") != 0) {
     delete c;
     return nullptr;
   }
@@ -621,6 +635,7 @@ void tclb_dist_ctx_destroy(void* ctx) {
   if (c->dsig) (void)hipFree(c->dsig);
   if (c->ready) (void)hipEventDestroy(c->ready);
   if (c->done) (void)hipEventDestroy(c->done);
+  if (c->fence) (void)hipEventDestroy(c->fence);
   if (c->cs) (void)hipStreamDestroy(c->cs);
   delete c;
 }

@@ -13,6 +13,14 @@
 
 namespace {
 
+__global__ void __launch_bounds__(256) k_acc_slots(double* a, int n6, int k) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n6) return;
+  double s = a[j];
+  for (int q = 1; q < k; q++) s += a[(long long)q * n6 + j];
+  a[j] = s;
+}
+
 __global__ void __launch_bounds__(256) k_nan_to_zero(double* a, int n) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n && isnan(a[i])) a[i] = 0.0;
@@ -213,6 +221,14 @@ int tclb_part_build_tree(const double* P, int n, int* grid, int nl, double mscal
     const int st = (1 << lvl) - 1, cnt = 1 << lvl;
     k_tree_level<<<(cnt + 255) / 256, 256, 0, s>>>(B, st, cnt);
   }
+  return (int)hipGetLastError();
+}
+
+// the k accumulator copies of the particle stage (core.hpp particle_acc) summed into the
+// first: acc[j] += acc[s * n6 + j], s = 1 .. k-1
+int tclb_part_acc_slots(double* acc, int n6, int k, void* stream) {
+  if (k <= 1 || n6 <= 0) return 0;
+  k_acc_slots<<<(n6 + 255) / 256, 256, 0, (hipStream_t)stream>>>(acc, n6, k);
   return (int)hipGetLastError();
 }
 

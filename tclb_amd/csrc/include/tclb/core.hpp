@@ -299,7 +299,8 @@ TCLB_FN void store_stream(T* p, T v) {
 // ---------------------------------------------------------------------------
 // Particles coupled to the lattice (reference Particle.hpp / RemoteForceInterface).
 // Device record (double): pos[3] vel[3] angvel[3] rad  -> PART_STRIDE = 10, in Launch.ext[2];
-// force/moment accumulators double[n][6] in Launch.ext[3].
+// force/moment accumulators double[n][6] in Launch.ext[3] (Launch.next[3] copies on the GPU,
+// particle_acc).
 // ---------------------------------------------------------------------------
 constexpr int PART_STRIDE = 10;
 
@@ -329,6 +330,23 @@ struct ParticleS {
     moment.z -= f.x * diff.y - f.y * diff.x;
   }
 };
+
+// The accumulator copy a node adds into: Launch.next[3] copies of the [n][6] block (0 or 1:
+// one), picked by the work-group on the GPU — the nodes a particle covers all add to the
+// same 6 doubles, and one copy serialised those atomics (the part256 force stage ran
+// 110-140 us of which ~20 us are its stores; profiles/README.md r06).  The copies are
+// summed into the first after the stage (tclb_part_acc_slots).
+TCLB_FN double* particle_acc(const Launch& L) {
+  double* acc = (double*)L.ext[3];
+#if TCLB_GPU && defined(__HIP_DEVICE_COMPILE__)
+  const long long k = L.next[3];
+  if (acc != nullptr && k > 1) {
+    const unsigned b = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+    acc += (long long)(b % (unsigned)k) * L.next[2] * 6;
+  }
+#endif
+  return acc;
+}
 
 // Flush one particle's force/moment contribution of this node.  On the GPU, when the
 // whole wavefront is active the 6 values are reduced across the wave first (one atomic

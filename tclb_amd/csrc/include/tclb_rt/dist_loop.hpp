@@ -148,7 +148,7 @@ struct PartPlan {
   int periodic;              // bit d: periodic along axis d
   int integrate;             // 1: SimplePart rigid step after the stage (not in Init)
   int allreduce;             // 1: sum the accumulator over the ranks after the stage
-  int reserved;
+  int nslots;                // accumulator copies (core.hpp particle_acc; GPU), summed after
   void* accbuf;              // IPC transport: this rank's shared copy of the accumulator
   const double* const* accs; // and every rank's, mapped (device array of nranks pointers)
 };

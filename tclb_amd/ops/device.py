@@ -32,6 +32,8 @@ def lib():
             P, i, d = ctypes.c_void_p, ctypes.c_int, ctypes.c_double
             L.tclb_part_nan_to_zero.argtypes = [P, i, P]
             L.tclb_part_nan_to_zero.restype = i
+            L.tclb_part_acc_slots.argtypes = [P, i, i, P]
+            L.tclb_part_acc_slots.restype = i
             L.tclb_part_rigid_step.argtypes = [P, P, P, P, i, d, d, d, i, d, d, d, P]
             L.tclb_part_rigid_step.restype = i
             L.tclb_part_build_grid.argtypes = [P, i, P, i, i, i, i, i, P, ctypes.c_longlong, P]
@@ -56,6 +58,11 @@ def _check(r: int, what: str):
 def nan_to_zero(t, stream: int):
     """t (contiguous fp64 device tensor): NaN -> 0 in place"""
     _check(lib().tclb_part_nan_to_zero(t.data_ptr(), t.numel(), stream), "particle NaN guard")
+
+
+def acc_slots(acc, n6: int, nslots: int, stream: int):
+    """the accumulator copies of a particle stage summed into the first (core.hpp particle_acc)"""
+    _check(lib().tclb_part_acc_slots(acc.data_ptr(), int(n6), int(nslots), stream), "particle accumulator copies")
 
 
 def rigid_step(P, acc, m, free, n: int, a, periodic: int, period, stream: int):

@@ -96,7 +96,7 @@ class PartPlan(ctypes.Structure):
                 ("ncell", ctypes.c_int), ("nl", ctypes.c_int), ("mscale", ctypes.c_double),
                 ("tmp", ctypes.c_void_p), ("tmp_bytes", ctypes.c_longlong), ("a", ctypes.c_double * 3),
                 ("period", ctypes.c_double * 3), ("periodic", ctypes.c_int), ("integrate", ctypes.c_int),
-                ("allreduce", ctypes.c_int), ("reserved", ctypes.c_int), ("accbuf", ctypes.c_void_p),
+                ("allreduce", ctypes.c_int), ("nslots", ctypes.c_int), ("accbuf", ctypes.c_void_p),
                 ("accs", ctypes.c_void_p)]
 
 
@@ -738,6 +738,7 @@ class NativeLoop:
                 Q.a[k], Q.period[k] = float(integ["a"][k]), float(integ["period"][k])
             Q.periodic = int(integ["periodic"])
         Q.allreduce = 1 if (lat.comm.distributed and lat.comm.size > 1) else 0
+        Q.nslots = d.get("nslots", 1)
         if Q.allreduce and self.gpu and self.transport == "ipc":
             Q.accbuf, Q.accs = self._ipc_acc(max(n, 1))
         keep.append(Q)

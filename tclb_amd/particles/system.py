@@ -95,7 +95,10 @@ class ParticleSystem:
         rec = np.zeros((max(1, n), PART_STRIDE))
         if n:
             rec[:n, 0:3], rec[:n, 3:6], rec[:n, 6:9], rec[:n, 9] = h["x"], h["v"], h["omega"], h["r"]
-        acc = np.zeros((max(1, n), 6))
+        # GPU: nslots copies of the accumulator (core.hpp particle_acc), enough to spread
+        # one particle's atomics over the work-groups, few when there are many particles
+        nslots = max(1, min(64, 4096 // max(1, n))) if dev.type == "cuda" else 1
+        acc = np.zeros((max(1, n) * nslots, 6))
         if n:
             acc[:n, 0:3], acc[:n, 3:6] = h["force"], h["torque"]
         d = {"P": torch.as_tensor(rec).to(dev), "acc": torch.as_tensor(acc).to(dev),
@@ -103,6 +106,7 @@ class ParticleSystem:
              "m": torch.as_tensor(np.where(h["m"] > 0, h["m"], 1.0) if n else np.ones(1)).to(dev),
              "free": torch.as_tensor(~h["fixed"] if n else np.zeros(1, dtype=bool)).to(dev)}
         d["grid"], d["cell"], d["kind"] = None, 1, None
+        d["nslots"] = nslots
         if self.container == "tree" and n >= 1:
             nl = 1 << (n - 1).bit_length()
             d["kind"], d["nl"] = "tree", nl
@@ -242,12 +246,13 @@ class ParticleSystem:
         """host bookkeeping after n native steps"""
         self._host_stale |= {"force", "torque"}
 
-    def _attach(self, lat, acc):
+    def _attach(self, lat, acc, nslots: int = 1):
         d = self._d
         L = lat._L
         L.ext[2] = d["P"].data_ptr()
         L.ext[3] = acc.data_ptr()
         L.next[2] = self.n
+        L.next[3] = nslots
         if d["grid"] is not None:
             self._build_native(lat)
             L.ext[4] = d["grid"].data_ptr()
@@ -261,7 +266,7 @@ class ParticleSystem:
         """before a particle stage: zero the accumulator, hand the records to the launch"""
         self._ensure(lat)
         self._d["acc"].zero_()
-        self._attach(lat, self._d["acc"])
+        self._attach(lat, self._d["acc"], self._d["nslots"])
 
     def attach_for_quantity(self, lat):
         """before a quantity launch (quantities may look at particles): the current
@@ -271,7 +276,11 @@ class ParticleSystem:
         self._attach(lat, self._d["qacc"])
 
     def post_stage(self, lat):
-        acc = self._d["acc"]
+        d = self._d
+        acc = d["acc"][:max(1, self.n)]
+        if d["nslots"] > 1 and self.n:
+            from ..ops import device as D
+            D.acc_slots(d["acc"], 6 * self.n, d["nslots"], lat._stream())
         if lat.comm.distributed and lat.comm.size > 1:
             acc.copy_(lat.comm.allreduce_globals(acc.reshape(-1).clone(), acc.numel()).reshape(acc.shape))
         # a NaN force is dropped (reference Lattice.cu.Rt:420-435 zeroes it with a notice;
@@ -288,6 +297,7 @@ class ParticleSystem:
     def detach(self, lat):
         """drop the particle records from the launch (after a stage or a quantity)"""
         lat._L.next[2] = 0
+        lat._L.next[3] = 0
         lat._L.ext[4] = None
         lat._L.next[4] = 0
 
