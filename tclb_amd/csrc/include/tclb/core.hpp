@@ -331,6 +331,17 @@ struct ParticleS {
   }
 };
 
+// A particle is certainly out of reach of node (x, y, z) — farther than its cut-off
+// rad + 2 (ParticleLoop / ParticleScan) — by an fp32 squared distance against a cut-off
+// widened by 1 % + 1 node: fp32 rounding of the coordinates (|x| < 2^24) cannot flip a
+// node inside the exact fp64 test to "far".  The exact test follows for the rest.
+TCLB_FN bool particle_far(const double* P, int i, int x, int y, int z) {
+  const double* p = P + (long long)i * PART_STRIDE;
+  const float dx = (float)x - (float)p[0], dy = (float)y - (float)p[1], dz = (float)z - (float)p[2];
+  const float c = (float)p[9] * 1.01f + 3.0f;
+  return dx * dx + dy * dy + dz * dz > c * c;
+}
+
 // The accumulator copy a node adds into: Launch.next[3] copies of the [n][6] block (0 or 1:
 // one), picked by the work-group on the GPU — the nodes a particle covers all add to the
 // same 6 doubles, and one copy serialised those atomics (the part256 force stage ran

@@ -77,3 +77,40 @@ def worker(rank, world, port, case, shape, steps, out, grid=None):
                        "part": parts[0][5]}, f)
     dist.barrier()
     dist.destroy_process_group()
+
+
+def worker_dead_peer(rank, world, port, out):
+    """rank 1 stops stepping after the first iterate; rank 0's next waits run into the
+    bounded IPC timeout and NativeLoop.wait raises instead of hanging (no collective
+    after that)"""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    os.environ["TCLB_DIST_TRANSPORT"] = "ipc"
+    os.environ["TCLB_IPC_TIMEOUT_S"] = "3"
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from tclb_amd.parallel.comm import TorchDistComm
+    from tclb_amd.parallel.native import NativeDistError
+    comm = TorchDistComm()
+    lat = run_case("d3q27", (32, 16, 24), 1, comm)
+    torch.cuda.synchronize()
+    dist.barrier()
+    import time
+    if rank == 1:
+        # a peer that stops stepping (stays alive, so the memory rank 0 has mapped stays
+        # valid) until the survivor has reported
+        t0 = time.time()
+        while not os.path.exists(out) and time.time() - t0 < 120:
+            time.sleep(0.2)
+        os._exit(0)
+    t0 = time.time()
+    msg = "no error"
+    try:
+        lat.iterate(3, glob_last=False)
+        lat._dist.wait()
+    except NativeDistError as e:
+        msg = str(e)
+    with open(out + ".tmp", "w") as f:
+        json.dump({"error": msg, "seconds": time.time() - t0}, f)
+    os.replace(out + ".tmp", out)
+    os._exit(0)                           # the group is out of step: no teardown

@@ -108,3 +108,24 @@ def test_ipc_loopback_one_rank(monkeypatch):
     assert lat._dist is not None and lat._dist.transport == "ipc"
     lat._dist.wait()
     assert torch.equal(lat.fields_interior(), ref.fields_interior())
+
+
+def test_ipc_dead_peer_times_out(tmp_path):
+    """a peer that stops stepping: the survivor's bounded waits time out (3 s, later waits
+    return at once), the wait after the steps raises NativeDistError, and the GPU queue
+    drains — no hang (a dead peer must raise, not hang the rank)"""
+    import torch.multiprocessing as mp
+    import ipc_worker
+    out = str(tmp_path / "dead.json")
+    ctx = mp.start_processes(ipc_worker.worker_dead_peer, args=(2, _port(), out), nprocs=2, start_method="spawn",
+                             join=False)
+    t0 = time.time()
+    while not ctx.join(timeout=5):
+        if time.time() - t0 > 180:
+            for p in ctx.processes:
+                if p.is_alive():
+                    p.kill()
+            pytest.fail("the surviving rank hung")
+    res = json.load(open(out))
+    assert "timed out" in res["error"], res
+    assert res["seconds"] < 60, res
