@@ -30,8 +30,9 @@ def collision_check(lat, action: str = "Iteration", min_rel: float = 1e-12, _fla
     with a COLLISION-group bit, 'mode'}; one extra step each with and without the collision
     bits.  When clearing them changes nothing, the bits either select no collision (the
     r04r case: flagged BGK on an MRT build — not the physics) or do not matter to this
-    model at all (its Run() acts on every node): every COLLISION type of the model is then
-    tried, and only if none of them matters does dynamics_check decide."""
+    model at all (its Run() acts on every node, e.g. a default collision branch); that is
+    decided by dynamics_check: the step's streamed populations must differ from pure
+    streaming of a non-uniform state."""
     m = lat.model
     mask = m.group_masks.get("COLLISION", 0)
     nx, ny, nz = lat.shape
@@ -90,13 +91,6 @@ def collision_check(lat, action: str = "Iteration", min_rel: float = 1e-12, _fla
         del probe
     out = {"collides": bool(rel > min_rel), "rel_diff": rel, "collision_nodes": coll_frac, "mode": "flags"}
     if not out["collides"] and _fallback:
-        for t in m.node_types:
-            if t.group != "COLLISION":
-                continue
-            tv = t.value - 0x10000 if (lat.flags.dtype == torch.int16 and t.value >= 0x8000) else t.value
-            alt = (orig_flags & keep) | tv
-            if collision_check(lat, action, min_rel, _flags=alt, _fallback=False)["collides"]:
-                return out       # the bits matter to this model; the configured ones collide nowhere
         # no COLLISION group, or a Run() that collides whatever the bits say (reaction /
         # diffusion systems, cm_cht, the finite-difference PDEs): the step must not be
         # pure streaming of a NON-uniform state
@@ -120,6 +114,12 @@ def dynamics_check(lat, action: str = "Iteration", min_rel: float = 1e-12) -> Di
         i = next((k for k, f in enumerate(m.fields) if f is dn.field or f.name == dn.field.name), None)
         if i is not None:
             shift[i] = (dn.dz, dn.dy, dn.dx)
+    # the streamed populations only, where the model has any: a macroscopic field computed
+    # by a later stage (a phase field summed from h) changes under pure streaming too, and
+    # would pass a run whose flags select no collision (the r04r case)
+    moving = [i for i in saved if i in shift and shift[i] != (0, 0, 0)]
+    if moving:
+        saved = moving
     state = lat.snaps[lat.cur].clone()
     other = lat.snaps[1 - lat.cur].clone() if m.late_reads(action) else None
     it, cur, glob = lat.iter, lat.cur, dict(lat.globals)

@@ -61,3 +61,31 @@ def test_perf_models_rejects_a_stream_only_run():
     assert good.returncode == 0, good.stderr[-2000:]
     rec = json.loads([l for l in good.stdout.splitlines() if l.startswith("{")][0])
     assert rec["collides"] is True and rec["valid"] is True
+
+
+def _lat2(name, flag=None, n=48):
+    lat = Lattice(name, (n, n, 1), device=torch.device("cpu"))
+    m = lat.model
+    t = m.node_type(flag) if flag else next((x for x in m.node_types if x.group == "COLLISION"), None)
+    lat.set_flags(np.full((lat.NZ, lat.NY, n), t.value if t else 0, dtype=np.uint32))
+    for k, v in case_settings(name).items():
+        if not k.startswith("_") and m.setting(k) is not None:
+            lat.set_setting(k, v)
+    lat.init()
+    lat.iterate(2)
+    return lat
+
+
+@pytest.mark.parametrize("name,flag,collides,mode", [
+    ("d2q9_reaction_diffusion_system_SIR_ModifiedPeng", "SRT_DF", True, "dynamics"),   # Run's default branch
+    ("d2q9_reaction_diffusion_system_SimpleDiffusion", "TRT_M", True, None),
+    ("diffusion2D", None, True, "dynamics"),               # no COLLISION group: a stencil update
+    ("wave2D", None, True, "dynamics"),
+    ("d2q9q9_cm_cht", "CM", False, "dynamics"),            # a type Run() has no case for: streaming only
+    ("d2q9q9_cm_cht", "CM_HIGHER", True, "flags"),
+])
+def test_guard_models_without_flag_dispatch(name, flag, collides, mode):
+    """models whose Run() does not select the collision by the COLLISION bits are judged
+    by one step from a non-uniform state against pure streaming of its populations"""
+    g = collision_check(_lat2(name, flag))
+    assert g["collides"] is collides and mode in (None, g["mode"]), g
