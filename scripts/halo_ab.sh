@@ -41,6 +41,8 @@ catalog)
   step "catalog fp64" 1100 $O/catalog_perf.jsonl python tools/perf_models.py --n3 256 --n2 2048 --steps 100 --allow-invalid ;;
 headline)
   step "bench fp64" 300 $O/bench_fp64.json python bench.py ;;
+peng)
+  step "SIR_ModifiedPeng guard" 300 $O/peng.jsonl python tools/perf_models.py --models d2q9_reaction_diffusion_system_SIR_ModifiedPeng,d2q9_reaction_diffusion_system_SIR_ModifiedPeng_Euler,d2q9_reaction_diffusion_system_SIR_ModifiedPeng_Heun,d2q9_reaction_diffusion_system_SIR_ModifiedPeng_Midpoint,d2q9_reaction_diffusion_system_SIR_ModifiedPeng_Trapezoidal --n2 2048 --steps 100 ;;
 cavitycounters)
   step "counters cavity fp64" 500 $O/counters_cavity.log python tools/counters.py --tag cavity_fp64 --nodes 16777216 --outdir $O/counters -- python3 $R/tools/bench_configs.py --configs cavity --steps 5 --warmup 1 ;;
 part)
