@@ -45,6 +45,12 @@ peng)
   step "SIR_ModifiedPeng guard" 300 $O/peng.jsonl python tools/perf_models.py --models d2q9_reaction_diffusion_system_SIR_ModifiedPeng,d2q9_reaction_diffusion_system_SIR_ModifiedPeng_Euler,d2q9_reaction_diffusion_system_SIR_ModifiedPeng_Heun,d2q9_reaction_diffusion_system_SIR_ModifiedPeng_Midpoint,d2q9_reaction_diffusion_system_SIR_ModifiedPeng_Trapezoidal --n2 2048 --steps 100 ;;
 cavitycounters)
   step "counters cavity fp64" 500 $O/counters_cavity.log python tools/counters.py --tag cavity_fp64 --nodes 16777216 --outdir $O/counters -- python3 $R/tools/bench_configs.py --configs cavity --steps 5 --warmup 1 ;;
+calcf)
+  for r in 16 2 0.5; do
+    step "calcf radius $r" 300 $O/calcf_$r.log rocprofv3 --kernel-trace --stats -d $O/calcf_$r -o run --output-format csv -- python3 $R/tools/calcf_probe.py --radius $r --steps 20
+  done ;;
+partcounters)
+  step "counters part256 fp64" 500 $O/counters_part256.log python tools/counters.py --tag part256_fp64 --nodes 16777216 --outdir $O/counters -- python3 $R/tools/bench_configs.py --configs part256 --steps 5 --warmup 1 ;;
 part)
   step "part256 fp64" 300 $O/part256_fp64.jsonl python tools/bench_configs.py --configs part256 --steps 100 --warmup 10
   step "rocprof part256" 400 $O/prof_part256.log rocprofv3 --kernel-trace --stats -d $O/prof_part256 -o run --output-format csv -- python3 $R/tools/bench_configs.py --configs part256 --steps 20 --warmup 2 ;;

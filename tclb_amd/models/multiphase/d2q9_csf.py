@@ -141,4 +141,11 @@ def build(bc=False, bcinit=False, noflow=False, weno=False, viscstep=False, cumu
     m.add_codegen(blocks)
     m.set_dynamics("multiphase/d2q9_csf.inc")
     m.glob_waves = 0 if weno else 2                  # WENO/cumulant: 326-334 VGPRs
+    if not (cumulant or weno):
+        # 2-wave occupancy floor on the stage kernels: the collision lands at 262 registers
+        # (1 wave/SIMD, latency-bound on its fp64 divisions and square roots); capped at
+        # 256 it spills 12 bytes and runs 0.613 -> 0.434 ms per 2048^2 step
+        # (profiles/README.md r06i).  The cumulant / WENO builds sit far above 256: a cap
+        # would spill heavily.
+        m.hip_flags = ["-DTCLB_STAGE_WAVES=2"]
     return m
