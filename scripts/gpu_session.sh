@@ -8,6 +8,27 @@ step() { local name=$1 t=$2 log=$3; shift 3; echo "== $name"; timeout -k 10 $t "
 export TMPDIR=/tmp
 for W in "$@"; do case $W in
 newtests) step "new gpu tests" 400 $O/pytest_gpu_new.log python -u -m pytest tests/test_gpu_oracles.py tests/test_gpu_kernels.py -v -m gpu --timeout 120 --timeout-method thread ;;
+slabscan)
+  # per-node cost against the z extent (one rank, one launch per step): where the 8-GPU
+  # slab loses to the full lattice
+  for nz in 64 128 256 512; do
+    step "plain 512x512x$nz fp64" 300 $O/slabscan_$nz.json python bench.py --shape 512,512,$nz --steps 100 --warmup 10
+  done
+  for k in 0 1 3 4; do
+    step "plain 512x512x64 fp64 tile split $k" 300 $O/slabscan_64_ts$k.json env TCLB_TILE_SPLIT=$k python bench.py --shape 512,512,64 --steps 100 --warmup 10
+  done
+  step "plain 512x512x64 fp64 no placement probe" 300 $O/slabscan_64_noplace.json env TCLB_PLACE=0 python bench.py --shape 512,512,64 --steps 100 --warmup 10
+  step "rocprof slab 64" 400 $O/prof_slab64.log rocprofv3 --kernel-trace --stats -d $O/prof_slab64 -o run --output-format csv -- python3 $R/bench.py --shape 512,512,64 --steps 100 --warmup 10 ;;
+tepsm6)
+  step "defer + split + tePSM GPU tests" 600 $O/pytest_defer.log python -u -m pytest tests/test_defer_stage.py tests/test_split_stage.py tests/test_tepsm.py -v -m gpu --timeout 120 --timeout-method thread
+  step "tePSM 256 fp64 uniform" 600 $O/tepsm_256.jsonl python tools/perf_models.py --models d3q27_tePSM_per_NEBB,d3q27_tePSM_per_SUP --n3 256 --steps 100 --rounds 2
+  step "tePSM 256 8 particles" 600 $O/tepsm256_cfg.jsonl python tools/bench_configs.py --configs tepsm256 --steps 100 --warmup 5
+  step "rocprof tePSM 8 particles" 400 $O/prof_tepsm256.log rocprofv3 --kernel-trace --stats -d $O/prof_tepsm256 -o run --output-format csv -- python3 $R/tools/bench_configs.py --configs tepsm256 --steps 20 --warmup 2 ;;
+calcf)
+  # the part256 force stage against the particle's size and count (kernel trace per case)
+  for c in "2 1" "8 1" "16 1" "16 4"; do set -- $c
+    step "calcf r=$1 n=$2" 300 $O/calcf_r$1_n$2.log rocprofv3 --kernel-trace --stats -d $O/calcf_r$1_n$2 -o run --output-format csv -- python3 $R/tools/calcf_probe.py --radius $1 --nparticles $2 --steps 40
+  done ;;
 tests) step "gpu tests" 900 $O/pytest_gpu.log python -u -m pytest tests -v -m gpu --timeout 120 --timeout-method thread ;;
 bench)
   step "bench fp64" 300 $O/bench_fp64.json python bench.py

@@ -133,8 +133,10 @@ __device__ __forceinline__ uint3 tile_id(const Launch& L) {
 // CLS: node class of a split stage (DSL add_stage(split=True), Node::node_class_): 1 / 2
 // run only the nodes of that class, each kernel compiled with that class's path alone;
 // 0 = every node (the stages that are not split)
+// dflag (class-1 kernels of a deferring stage, k_stage_defer): set when a node of the
+// tile was handed to the CLS 3 kernel (Node::defer_heavy)
 template <class Model, class R, class S, int STG, bool GLOB, int CLS = 0>
-__device__ __forceinline__ void stage_tile(const Launch& L, const uint3 t) {
+__device__ __forceinline__ void stage_tile(const Launch& L, const uint3 t, int* dflag = nullptr) {
   typedef typename Model::template NodeCls<R, S, GLOB, CLS> N;
   typedef typename N::G_ G;   // fp64 accumulators, also in fp32-compute builds (core.hpp glob_acc)
   const int x = L.xlo + (int)(t.x * blockDim.x + threadIdx.x);
@@ -157,6 +159,9 @@ __device__ __forceinline__ void stage_tile(const Launch& L, const uint3 t) {
     if (x < L.xhi && y < L.yhi) {
       N n(L, x, y, z, g);
       n.template run_stage<STG>();
+      if constexpr (CLS == 1 && Model::defer_stage(STG)) {
+        if (dflag && n.deferred_) *dflag = 1;
+      }
     }
     block_globals_regs<NG, Model::NSUMGLOBALS_>(g, L.globals);
   } else if constexpr (GLOB) {
@@ -166,6 +171,9 @@ __device__ __forceinline__ void stage_tile(const Launch& L, const uint3 t) {
     if (x < L.xhi && y < L.yhi) {
       N n(L, x, y, z, acc);
       n.template run_stage<STG>();
+      if constexpr (CLS == 1 && Model::defer_stage(STG)) {
+        if (dflag && n.deferred_) *dflag = 1;
+      }
     }
     block_globals_flush<NG, Model::NSUMGLOBALS_>(acc, L.globals);
   } else {
@@ -173,6 +181,9 @@ __device__ __forceinline__ void stage_tile(const Launch& L, const uint3 t) {
     if (x < L.xhi && y < L.yhi) {
       N n(L, x, y, z, g);
       n.template run_stage<STG>();
+      if constexpr (CLS == 1 && Model::defer_stage(STG)) {
+        if (dflag && n.deferred_) *dflag = 1;
+      }
     }
   }
 }
@@ -279,6 +290,7 @@ struct ClassTiles {
   int box[6];
   unsigned bx, by;
   unsigned* list;   // device: the class-1 tiles, then the class-2 tiles
+  unsigned* dq;     // deferring stages: [count][class-1 tiles handed to the CLS 3 kernel]
   unsigned n1, n2, total;
   unsigned long long used;
 };
@@ -307,6 +319,7 @@ inline bool class_tiles(const Launch& L, dim3 grid, dim3 block, hipStream_t s, C
   for (size_t i = 0; i < cache.size();) {
     if (cache[i].flags == L.flags && cache[i].gen != L.flags_gen) {
       hipFree(cache[i].list);
+      hipFree(cache[i].dq);
       cache.erase(cache.begin() + (long)i);
     } else {
       i++;
@@ -317,6 +330,7 @@ inline bool class_tiles(const Launch& L, dim3 grid, dim3 block, hipStream_t s, C
     for (size_t i = 1; i < cache.size(); i++)
       if (cache[i].used < cache[o].used) o = i;
     hipFree(cache[o].list);
+    hipFree(cache[o].dq);
     cache.erase(cache.begin() + (long)o);
   }
   const unsigned total = grid.x * grid.y * grid.z;
@@ -345,11 +359,17 @@ inline bool class_tiles(const Launch& L, dim3 grid, dim3 block, hipStream_t s, C
   c.total = total;
   c.used = ++clock;
   c.list = nullptr;
+  c.dq = nullptr;
+  if (Model::defer_stage(STG) && hipMalloc(&c.dq, (l1.size() + 1) * sizeof(unsigned)) != hipSuccess) return false;
   l1.insert(l1.end(), l2.begin(), l2.end());
   if (!l1.empty()) {
-    if (hipMalloc(&c.list, l1.size() * sizeof(unsigned)) != hipSuccess) return false;
+    if (hipMalloc(&c.list, l1.size() * sizeof(unsigned)) != hipSuccess) {
+      hipFree(c.dq);
+      return false;
+    }
     if (hipMemcpy(c.list, l1.data(), l1.size() * sizeof(unsigned), hipMemcpyHostToDevice) != hipSuccess) {
       hipFree(c.list);
+      hipFree(c.dq);
       return false;
     }
   }
@@ -367,6 +387,36 @@ template <class Model, class R, class S, int STG, bool GLOB, int W, int CLS>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W)))
 k_stage_list_w(const Launch L, const unsigned* list, unsigned n, unsigned gx, unsigned gy) {
   stage_tile<Model, R, S, STG, GLOB, CLS>(L, list_tile(L, list, n, gx, gy));
+}
+
+// Deferring split stages (DSL add_stage(defer=True)).  The class-1 kernel queues every
+// tile in which a node took Node::defer_heavy (one atomic per such work-group); the CLS 3
+// kernel then runs only the queued tiles, with a grid of at most DEFER_GRID work-groups
+// that stride over the queue (its length is read once, after the class-1 kernel ended:
+// every work-group reaches the end of the queue).  The rare heavy branch is compiled
+// into the CLS 3 kernel alone, so it no longer sets the class-1 kernel's register budget
+// (d3q27_tePSM_per: the CHT interface closure, 438 -> 242 registers, 1 -> 2 waves/SIMD).
+constexpr unsigned DEFER_GRID = 2048;
+template <class Model, class R, class S, int STG, bool GLOB, int W>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W > 0 ? W : 1)))
+k_stage_defer(const Launch L, const unsigned* list, unsigned n, unsigned gx, unsigned gy, unsigned* dq) {
+  __shared__ int dflag;
+  const bool lead = threadIdx.x == 0 && threadIdx.y == 0;
+  if (lead) dflag = 0;
+  __syncthreads();
+  const uint3 t = list_tile(L, list, n, gx, gy);
+  stage_tile<Model, R, S, STG, GLOB, 1>(L, t, &dflag);
+  __syncthreads();
+  if (lead && dflag) dq[1 + atomicAdd(dq, 1u)] = t.x + gx * (t.y + gy * t.z);
+}
+template <class Model, class R, class S, int STG, int W>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W > 0 ? W : 1)))
+k_stage_deferred(const Launch L, const unsigned* dq, unsigned gx, unsigned gy) {
+  const unsigned cnt = dq[0];
+  for (unsigned i = blockIdx.x; i < cnt; i += gridDim.x) {
+    const unsigned b = dq[1 + i];
+    stage_tile<Model, R, S, STG, false, 3>(L, make_uint3(b % gx, (b / gx) % gy, b / (gx * gy)));
+  }
 }
 
 // LDS-staged stencil tiles: csrc/include/tclb_tile/k_tile.hpp (a dependency of the
@@ -464,8 +514,25 @@ inline bool launch_one(const Launch& L, dim3 grid, dim3 block, hipStream_t s) {
     // tiles that hold nodes of its class
     ClassTiles c;
     const ClassTiles* ct = class_tiles<Model, R, S, I>(L, grid, block, s, c) ? &c : nullptr;
-    launch_class<Model, R, S, I, G, 1>(L, grid, block, s, ct);
-    launch_class<Model, R, S, I, G, 2>(L, grid, block, s, ct);
+    if constexpr (Model::defer_stage(I)) {
+      // class 1 (queueing the deferred tiles), the deferred nodes, then class 2; the
+      // queue lives with the tile lists (no lists: nothing to run the stage with)
+      if (!ct || !ct->dq) return false;
+      if (ct->n1 > 0) {
+        constexpr int W = (G && glob_waves<Model>() > 0) ? glob_waves<Model>() : TCLB_SPLIT_WAVES;
+        const unsigned* list = ct->n1 == ct->total ? nullptr : ct->list;
+        if (hipMemsetAsync(ct->dq, 0, sizeof(unsigned), s) != hipSuccess) return false;
+        k_stage_defer<Model, R, S, I, G, W><<<dim3(ct->n1), block, 0, s>>>(L, list, ct->n1, grid.x, grid.y, ct->dq);
+        // the heavy path under the class-2 floor (no AGPRs, the form measured right; its
+        // spills cost little on the few nodes it runs)
+        k_stage_deferred<Model, R, S, I, TCLB_SPLIT_WAVES2><<<dim3(ct->n1 < DEFER_GRID ? ct->n1 : DEFER_GRID), block, 0, s>>>(
+            L, ct->dq, grid.x, grid.y);
+      }
+      launch_class<Model, R, S, I, G, 2>(L, grid, block, s, ct);
+    } else {
+      launch_class<Model, R, S, I, G, 1>(L, grid, block, s, ct);
+      launch_class<Model, R, S, I, G, 2>(L, grid, block, s, ct);
+    }
     return true;
   }
   if constexpr (G && glob_waves<Model>() > 0) {

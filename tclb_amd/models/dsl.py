@@ -112,6 +112,8 @@ class Stage:
     split: bool = False       # GPU: two kernels by node class (Node::node_class_(): 1 =
                               # the common interior path, 2 = the rest), each compiled with
                               # its own path only and so its own register budget
+    defer: bool = False       # split stage whose class-1 path hands the nodes that need a
+                              # rare heavy branch to a third kernel (Node::defer_heavy)
     keep: Optional[List[str]] = None   # fields (nicenames / group tags) the stage leaves
                                        # unchanged and does not store; the lattice keeps
                                        # both snapshots' copies equal (Lattice._mirror_kept)
@@ -288,7 +290,7 @@ class Model:
                   save_fields=False, read_fields: Optional[Sequence[str]] = None,
                   fixed_point: bool = False, particle: bool = False, init: bool = False,
                   snapshot_reads: bool = False, lazy_load: bool = False, lds: Optional[Sequence[str]] = None,
-                  split: bool = False, keep: Optional[Sequence[str]] = None):
+                  split: bool = False, keep: Optional[Sequence[str]] = None, defer: bool = False):
         """AddStage (src/conf.R:295-330): load_densities / save_fields are True (all), False
         (none) or lists of field names / group tags (reference defaults: FALSE).
         lazy_load: the stage's main pulls its densities itself (load_<name>()), e.g. only
@@ -301,6 +303,13 @@ class Model:
         the executors that run every node in one pass), so a rare heavy path (boundary
         closures) does not set the register budget, and with it the occupancy, of the
         common one.
+        defer: (split stages) the class-1 node code may hand a node to a third kernel at
+        run time: defer_heavy(cond) is true, in the class-1 kernel, where the node needs the
+        heavy branch — the node is then not stored and its tile is queued — and, in that
+        third kernel (CLS_ 3, over the queued tiles only, no globals), where it does not.
+        So a heavy branch that depends on field values (e.g. a media interface that moves
+        with the particles) also leaves the common kernel's register budget.  Globals must
+        be added before the defer point.  CPU and unsplit executors: never defers.
         keep: entries of save_fields (same tags) that the stage never changes, e.g. wall
         normals set at initialisation: they are not stored (no read and write of them per
         node and step) and the lattice copies them into the other snapshot once before an
@@ -319,7 +328,9 @@ class Model:
                    read_fields=list(read_fields) if read_fields is not None else None,
                    fixed_point=fixed_point, particle=particle, init=init, snapshot_reads=snapshot_reads,
                    lazy_load=lazy_load, lds=list(lds) if lds else None, split=split,
-                   keep=list(keep) if keep else None)
+                   keep=list(keep) if keep else None, defer=defer)
+        if defer and not split:
+            raise ModelError(f"stage {name}: defer needs split=True")
         self.stages = [s for s in self.stages if s.name != name] + [st]
         return st
 

@@ -84,8 +84,11 @@ def build(nebb: bool = False, sup: bool = False, isothermal: bool = False) -> Mo
         calc_load = ["f", "Force", "l"]
     # the initial coverage (CalcPeriodicSolid in Init) needs the particles: particle stage
     m.add_stage("BaseInit", "Init", save_fields=groups, load_densities=groups, particle=True)
-    # split: the interior collision and the face closures run as two kernels
-    m.add_stage("BaseIteration", "Run", save_fields=groups, load_densities=groups, split=True)
+    # split: the interior collision and the face closures run as two kernels; defer: the
+    # CHT interface closure of the interior collision runs as a third, over the tiles
+    # whose nodes need it (they move with the particles)
+    m.add_stage("BaseIteration", "Run", save_fields=groups, load_densities=groups, split=True,
+                defer=not isothermal)
     # lazy: the populations are pulled only where a particle covers the node
     m.add_stage("CalcF", "CalcF", save_fields=["Force"], load_densities=calc_load, particle=True, lazy_load=True)
     m.add_action("Iteration", ["BaseIteration", "CalcF"])

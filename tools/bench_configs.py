@@ -99,6 +99,29 @@ def part256(shape, precision, dev, comm=None):
     return lat
 
 
+def tepsm256(shape, precision, dev, comm=None):
+    """thermal PSM (d3q27_tePSM_per_NEBB, f + h) in a periodic box with 8 fixed hot-spot
+    particles of radius n/16: their coverage makes a second medium, so every step has
+    CHT interface nodes around each sphere (the deferred kernel's work) besides the bulk"""
+    from tclb_amd.particles import SimplePart
+    nx, ny, nz = shape
+    lat = Lattice("d3q27_tePSM_per_NEBB", shape, device=dev, precision=precision, comm=comm)
+    m = lat.model
+    fl = np.full((lat.NZ, lat.NY, nx), m.node_type("BGK").value, dtype=np.uint32)
+    lat.set_flags(fl)
+    for k, v in dict(omegaF=1 / (3 * 0.05 + 0.5), FluidConductivity=0.1, SolidConductivity=0.3, SolidCv=2.0,
+                     SolidRho=2.0, AccelX=1e-6, DNx=nx, DNy=ny, DNz=nz, InitTemperature=0.5).items():
+        lat.set_setting(k, v)
+    ps = SimplePart()
+    r = nx / 16
+    for i in range(8):
+        c = ((i & 1) + 0.5, ((i >> 1) & 1) + 0.5, ((i >> 2) & 1) + 0.5)
+        ps.add([c[0] * nx / 2 + 0.3, c[1] * ny / 2 + 0.6, c[2] * nz / 2 + 0.2], r, fixed=True)
+    lat.particles = ps
+    lat.init()
+    return lat
+
+
 def physics_checks(lat) -> dict:
     """a timing only counts on a run that stayed physical: finite globals and fields;
     a particle's velocity finite and bounded"""
@@ -118,7 +141,8 @@ def physics_checks(lat) -> dict:
 
 CONFIGS = {"cavity": (cavity, 256, "d3q19 BGK lid-driven cavity 256^3"),
            "pf384": (pf384, 384, "d3q27 multiphase droplet 384^3 (two distribution sets)"),
-           "part256": (part256, 256, "d3q19 + moving particle 256^3")}
+           "part256": (part256, 256, "d3q19 + moving particle 256^3"),
+           "tepsm256": (tepsm256, 256, "d3q27 thermal PSM, 8 fixed particles, 256^3 (not a BASELINE config)")}
 
 
 def main():

@@ -7,7 +7,8 @@ class-0 instantiation only, so UBSan on the CPU build (tests/test_ubsan.py) neve
 the class forms.  This tool takes the state of a small case after `--steps` iterations
 (tests/model_cases.py make_case + perturb), dumps the launch and every buffer it points
 to, and builds a host driver with clang++ -fsanitize=memory that runs one stage over the
-whole box exactly as the GPU dispatch does: class 1 on every node, then class 2 (or the
+whole box exactly as the GPU dispatch does: class 1 on every node, then class 3 (the nodes a
+deferring stage's class 1 handed on), then class 2 (or the
 plain node for an unsplit stage; --cls 0 forces that).  Memory Sanitizer aborts on a branch
 on an uninitialised value, and after the stage every stored byte of the output snapshot is
 checked with __msan_test_shadow: a node that stores a value computed from an uninitialised
@@ -161,7 +162,9 @@ def main():
     sname = a.stage or m.action("Iteration").stages[0]
     si = m.stage_index(sname)
     split = bool(m.stage(sname).split)
-    classes = [1, 2] if (split and a.cls < 0) else [max(0, a.cls)]
+    # a deferring stage: class 1, its deferred nodes (CLS 3: executor_hip.hpp k_stage_deferred), class 2
+    seq = [1, 3, 2] if getattr(m.stage(sname), "defer", False) else [1, 2]
+    classes = seq if (split and a.cls < 0) else [max(0, a.cls)]
     tmp = a.keep or tempfile.mkdtemp(prefix="msan_")
     os.makedirs(tmp, exist_ok=True)
     capture(lat, si, a.glob, tmp)
