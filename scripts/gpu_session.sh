@@ -29,6 +29,31 @@ calcf)
   for c in "2 1" "8 1" "16 1" "16 4"; do set -- $c
     step "calcf r=$1 n=$2" 300 $O/calcf_r$1_n$2.log rocprofv3 --kernel-trace --stats -d $O/calcf_r$1_n$2 -o run --output-format csv -- python3 $R/tools/calcf_probe.py --radius $1 --nparticles $2 --steps 40
   done ;;
+part6)
+  step "particle / defer / ipc GPU tests" 600 $O/pytest_part.log python -u -m pytest tests/test_particles.py tests/test_bench_particle_case.py tests/test_gpu_ipc.py tests/test_defer_stage.py tests/test_catalog.py -k "part or defer or ipc or Particle or tePSM" -v -m gpu --timeout 120 --timeout-method thread
+  step "part256 fp64" 300 $O/part256_fp64.jsonl python tools/bench_configs.py --configs part256 --steps 100 --warmup 5
+  for t in plain rccl copy ipc; do
+    if [ $t = plain ]; then
+      step "part256 slab plain" 300 $O/part_slab_plain.jsonl python tools/bench_configs.py --configs part256 --shape 256,256,64 --steps 200 --warmup 10
+    else
+      step "part256 slab $t" 300 $O/part_slab_$t.jsonl python tools/bench_configs.py --configs part256 --shape 256,256,64 --loopback-dist --transport $t --steps 200 --warmup 10
+    fi
+  done ;;
+slabts)
+  for r in 1 2; do for nz in 64 128 256; do for k in 0 2; do
+    step "plain 512x512x$nz ts$k #$r" 300 $O/slabts_${nz}_ts${k}_$r.json env TCLB_TILE_SPLIT=$k python bench.py --shape 512,512,$nz --steps 100 --warmup 10
+  done; done; done ;;
+rcclenv)
+  # RCCL self-send on the 8-GPU headline slab against its channel count (the RCCL kernel's
+  # work-groups compete with the interior launch for CUs)
+  step "slab plain" 300 $O/rcclenv_plain.json python bench.py --shape 512,512,64 --steps 200 --warmup 20
+  step "slab rccl default" 300 $O/rcclenv_default.json python bench.py --shape 512,512,64 --steps 200 --warmup 20 --loopback-dist --transport rccl
+  for c in 1 2 4 8; do
+    step "slab rccl NCCL_MAX_NCHANNELS=$c" 300 $O/rcclenv_max$c.json env NCCL_MAX_NCHANNELS=$c NCCL_MIN_NCHANNELS=1 python bench.py --shape 512,512,64 --steps 200 --warmup 20 --loopback-dist --transport rccl
+  done
+  step "slab rccl NCCL_NCHANNELS_PER_PEER=1" 300 $O/rcclenv_pp1.json env NCCL_NCHANNELS_PER_PEER=1 python bench.py --shape 512,512,64 --steps 200 --warmup 20 --loopback-dist --transport rccl
+  step "slab ipc" 300 $O/rcclenv_ipc.json python bench.py --shape 512,512,64 --steps 200 --warmup 20 --loopback-dist --transport ipc
+  step "slab copy" 300 $O/rcclenv_copy.json python bench.py --shape 512,512,64 --steps 200 --warmup 20 --loopback-dist --transport copy ;;
 tests) step "gpu tests" 900 $O/pytest_gpu.log python -u -m pytest tests -v -m gpu --timeout 120 --timeout-method thread ;;
 bench)
   step "bench fp64" 300 $O/bench_fp64.json python bench.py

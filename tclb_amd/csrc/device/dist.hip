@@ -261,19 +261,40 @@ struct GpuSvc {
     return 0;
   }
 
+  // RCCL: every message goes as pieces of at most rccl_chunk() bytes, in order (both ends
+  // cut an op the same way, and sends / receives between a pair of ranks match in issue
+  // order).  With one channel per peer, whole 18.9 MB halves of the 512x512x64 d3q27 slab
+  // arrived wrong, deterministically, and 4.7 MB ones right (profiles/README.md r06n-o);
+  // the per-peer channel count RCCL picks between two GPUs is not known here, so no
+  // message is allowed to be large.
+  static size_t rccl_chunk() {
+    static const size_t b = [] {
+      const char* e = getenv("TCLB_RCCL_CHUNK_MB");
+      const double mb = e ? atof(e) : 4.0;
+      return mb > 0 ? (size_t)(mb * 1048576.0) : (size_t)0;   // 0: whole messages
+    }();
+    return b;
+  }
   int p2p(char* base, char* stg, const tclb::HaloOp* ops, int nops) {
     if (nops == 0) return 0;
     if (c->transport == 1) {
       int r;
+      const size_t chunk = rccl_chunk();
       if ((r = rccl_check(c, c->R.group_start(), "ncclGroupStart")) != 0) return r;
       for (int i = 0; i < nops; i++) {
         const tclb::HaloOp& o = ops[i];
         char* a = (o.buf ? stg : base) + o.off;
-        const int e = o.kind == 0 ? c->R.send(a, (size_t)o.bytes, 0, o.peer, c->comm, c->cs)
-                                  : c->R.recv(a, (size_t)o.bytes, 0, o.peer, c->comm, c->cs);
-        if (e != 0) {
-          c->R.group_end();
-          return rccl_check(c, e, o.kind == 0 ? "ncclSend" : "ncclRecv");
+        const size_t tot = (size_t)o.bytes;
+        for (size_t done = 0; done < tot || (tot == 0 && done == 0);) {
+          const size_t b = (chunk == 0 || tot - done <= chunk) ? tot - done : chunk;
+          const int e = o.kind == 0 ? c->R.send(a + done, b, 0, o.peer, c->comm, c->cs)
+                                    : c->R.recv(a + done, b, 0, o.peer, c->comm, c->cs);
+          if (e != 0) {
+            c->R.group_end();
+            return rccl_check(c, e, o.kind == 0 ? "ncclSend" : "ncclRecv");
+          }
+          done += b;
+          if (tot == 0) break;
         }
       }
       return rccl_check(c, c->R.group_end(), "ncclGroupEnd");

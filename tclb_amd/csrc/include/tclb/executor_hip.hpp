@@ -133,10 +133,27 @@ __device__ __forceinline__ uint3 tile_id(const Launch& L) {
 // CLS: node class of a split stage (DSL add_stage(split=True), Node::node_class_): 1 / 2
 // run only the nodes of that class, each kernel compiled with that class's path alone;
 // 0 = every node (the stages that are not split)
-// dflag (class-1 kernels of a deferring stage, k_stage_defer): set when a node of the
-// tile was handed to the CLS 3 kernel (Node::defer_heavy)
+// Deferring split stages: the node list of the CLS 3 pass, dq = [count][node ids] (id: the
+// node's linear index in the launch box).  The lanes of a wave that deferred reserve their
+// slots with one atomic (ballot + prefix count).
+__device__ __forceinline__ void defer_record(unsigned* dq, bool d, unsigned id) {
+  const unsigned long long m = __ballot(d);
+  if (m == 0ull) return;
+  const int lane = __lane_id();
+  const int leader = __ffsll((long long)m) - 1;
+  unsigned base = 0;
+  if (lane == leader) base = atomicAdd(dq, (unsigned)__popcll(m));
+  base = __shfl(base, leader, 64);
+  if (d) dq[1 + base + (unsigned)__popcll(m & ((1ull << lane) - 1ull))] = id;
+}
+__device__ __forceinline__ unsigned box_id(const Launch& L, int x, int y, int z) {
+  return ((unsigned)(z - L.zlo) * (unsigned)(L.yhi - L.ylo) + (unsigned)(y - L.ylo)) * (unsigned)(L.xhi - L.xlo) +
+         (unsigned)(x - L.xlo);
+}
+// dq (class-1 kernels of a deferring stage, k_stage_defer): where the nodes handed to the
+// CLS 3 pass (Node::defer_heavy) are recorded
 template <class Model, class R, class S, int STG, bool GLOB, int CLS = 0>
-__device__ __forceinline__ void stage_tile(const Launch& L, const uint3 t, int* dflag = nullptr) {
+__device__ __forceinline__ void stage_tile(const Launch& L, const uint3 t, unsigned* dq = nullptr) {
   typedef typename Model::template NodeCls<R, S, GLOB, CLS> N;
   typedef typename N::G_ G;   // fp64 accumulators, also in fp32-compute builds (core.hpp glob_acc)
   const int x = L.xlo + (int)(t.x * blockDim.x + threadIdx.x);
@@ -160,7 +177,7 @@ __device__ __forceinline__ void stage_tile(const Launch& L, const uint3 t, int* 
       N n(L, x, y, z, g);
       n.template run_stage<STG>();
       if constexpr (CLS == 1 && Model::defer_stage(STG)) {
-        if (dflag && n.deferred_) *dflag = 1;
+        if (dq) defer_record(dq, n.deferred_, box_id(L, x, y, z));
       }
     }
     block_globals_regs<NG, Model::NSUMGLOBALS_>(g, L.globals);
@@ -172,7 +189,7 @@ __device__ __forceinline__ void stage_tile(const Launch& L, const uint3 t, int* 
       N n(L, x, y, z, acc);
       n.template run_stage<STG>();
       if constexpr (CLS == 1 && Model::defer_stage(STG)) {
-        if (dflag && n.deferred_) *dflag = 1;
+        if (dq) defer_record(dq, n.deferred_, box_id(L, x, y, z));
       }
     }
     block_globals_flush<NG, Model::NSUMGLOBALS_>(acc, L.globals);
@@ -182,7 +199,7 @@ __device__ __forceinline__ void stage_tile(const Launch& L, const uint3 t, int* 
       N n(L, x, y, z, g);
       n.template run_stage<STG>();
       if constexpr (CLS == 1 && Model::defer_stage(STG)) {
-        if (dflag && n.deferred_) *dflag = 1;
+        if (dq) defer_record(dq, n.deferred_, box_id(L, x, y, z));
       }
     }
   }
@@ -290,7 +307,7 @@ struct ClassTiles {
   int box[6];
   unsigned bx, by;
   unsigned* list;   // device: the class-1 tiles, then the class-2 tiles
-  unsigned* dq;     // deferring stages: [count][class-1 tiles handed to the CLS 3 kernel]
+  unsigned* dq;     // deferring stages: [count][class-1 nodes handed to the CLS 3 kernel]
   unsigned n1, n2, total;
   unsigned long long used;
 };
@@ -360,7 +377,10 @@ inline bool class_tiles(const Launch& L, dim3 grid, dim3 block, hipStream_t s, C
   c.used = ++clock;
   c.list = nullptr;
   c.dq = nullptr;
-  if (Model::defer_stage(STG) && hipMalloc(&c.dq, (l1.size() + 1) * sizeof(unsigned)) != hipSuccess) return false;
+  // room for every node of the class-1 tiles (4 B per node)
+  if (Model::defer_stage(STG) &&
+      hipMalloc(&c.dq, ((size_t)l1.size() * block.x * block.y + 1) * sizeof(unsigned)) != hipSuccess)
+    return false;
   l1.insert(l1.end(), l2.begin(), l2.end());
   if (!l1.empty()) {
     if (hipMalloc(&c.list, l1.size() * sizeof(unsigned)) != hipSuccess) {
@@ -389,33 +409,34 @@ k_stage_list_w(const Launch L, const unsigned* list, unsigned n, unsigned gx, un
   stage_tile<Model, R, S, STG, GLOB, CLS>(L, list_tile(L, list, n, gx, gy));
 }
 
-// Deferring split stages (DSL add_stage(defer=True)).  The class-1 kernel queues every
-// tile in which a node took Node::defer_heavy (one atomic per such work-group); the CLS 3
-// kernel then runs only the queued tiles, with a grid of at most DEFER_GRID work-groups
-// that stride over the queue (its length is read once, after the class-1 kernel ended:
-// every work-group reaches the end of the queue).  The rare heavy branch is compiled
-// into the CLS 3 kernel alone, so it no longer sets the class-1 kernel's register budget
-// (d3q27_tePSM_per: the CHT interface closure, 438 -> 242 registers, 1 -> 2 waves/SIMD).
+// Deferring split stages (DSL add_stage(defer=True)).  The class-1 kernel records every
+// node that took Node::defer_heavy (defer_record); the CLS 3 kernel then runs only those,
+// one per thread of a grid of at most DEFER_GRID work-groups striding over the list (its
+// length is read once, after the class-1 kernel ended: every thread reaches its end).  The
+// rare heavy branch is compiled into the CLS 3 kernel alone, so it no longer sets the
+// class-1 kernel's register budget (d3q27_tePSM_per: the CHT interface closure, 438 ->
+// 254 registers, 1 -> 2 waves/SIMD), and its lanes are all busy (a list of nodes, not of
+// tiles: a tile with interface nodes has ~20 of 256).
 constexpr unsigned DEFER_GRID = 2048;
 template <class Model, class R, class S, int STG, bool GLOB, int W>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W > 0 ? W : 1)))
 k_stage_defer(const Launch L, const unsigned* list, unsigned n, unsigned gx, unsigned gy, unsigned* dq) {
-  __shared__ int dflag;
-  const bool lead = threadIdx.x == 0 && threadIdx.y == 0;
-  if (lead) dflag = 0;
-  __syncthreads();
-  const uint3 t = list_tile(L, list, n, gx, gy);
-  stage_tile<Model, R, S, STG, GLOB, 1>(L, t, &dflag);
-  __syncthreads();
-  if (lead && dflag) dq[1 + atomicAdd(dq, 1u)] = t.x + gx * (t.y + gy * t.z);
+  stage_tile<Model, R, S, STG, GLOB, 1>(L, list_tile(L, list, n, gx, gy), dq);
 }
+// the list holds any (x, y, z) per lane: the flat addressing form only (Node::ROWA_ assumes
+// a wave-uniform row)
 template <class Model, class R, class S, int STG, int W>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W > 0 ? W : 1)))
-k_stage_deferred(const Launch L, const unsigned* dq, unsigned gx, unsigned gy) {
+k_stage_deferred(const Launch L, const unsigned* dq) {
+  typedef typename Model::template NodeCls<R, S, false, 3> N;
+  static_assert(!N::ROWA_, "deferred nodes need the flat addressing form");
   const unsigned cnt = dq[0];
-  for (unsigned i = blockIdx.x; i < cnt; i += gridDim.x) {
-    const unsigned b = dq[1 + i];
-    stage_tile<Model, R, S, STG, false, 3>(L, make_uint3(b % gx, (b / gx) % gy, b / (gx * gy)));
+  const unsigned w = (unsigned)(L.xhi - L.xlo), h = (unsigned)(L.yhi - L.ylo);
+  for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < cnt; i += gridDim.x * blockDim.x) {
+    const unsigned id = dq[1 + i], r = id / w;
+    typename N::G_ g[1] = {typename N::G_(0)};
+    N nd(L, L.xlo + (int)(id % w), L.ylo + (int)(r % h), L.zlo + (int)(r / h), g);
+    nd.template run_stage<STG>();
   }
 }
 
@@ -525,8 +546,9 @@ inline bool launch_one(const Launch& L, dim3 grid, dim3 block, hipStream_t s) {
         k_stage_defer<Model, R, S, I, G, W><<<dim3(ct->n1), block, 0, s>>>(L, list, ct->n1, grid.x, grid.y, ct->dq);
         // the heavy path under the class-2 floor (no AGPRs, the form measured right; its
         // spills cost little on the few nodes it runs)
-        k_stage_deferred<Model, R, S, I, TCLB_SPLIT_WAVES2><<<dim3(ct->n1 < DEFER_GRID ? ct->n1 : DEFER_GRID), block, 0, s>>>(
-            L, ct->dq, grid.x, grid.y);
+        const unsigned long long cap = (unsigned long long)ct->n1 * block.x * block.y;
+        const unsigned dg = (unsigned)((cap + 255) / 256 < DEFER_GRID ? (cap + 255) / 256 : DEFER_GRID);
+        k_stage_deferred<Model, R, S, I, TCLB_SPLIT_WAVES2><<<dim3(dg), dim3(256), 0, s>>>(L, ct->dq);
       }
       launch_class<Model, R, S, I, G, 2>(L, grid, block, s, ct);
     } else {

@@ -309,7 +309,9 @@ class Model:
         third kernel (CLS_ 3, over the queued tiles only, no globals), where it does not.
         So a heavy branch that depends on field values (e.g. a media interface that moves
         with the particles) also leaves the common kernel's register budget.  Globals must
-        be added before the defer point.  CPU and unsplit executors: never defers.
+        be added before the defer point.  The node code also defines defer_pre_(stage): the
+        same test from what the node can read before the stage's loads (true when unsure),
+        which the CLS_ 3 kernel runs first.  CPU and unsplit executors: never defers.
         keep: entries of save_fields (same tags) that the stage never changes, e.g. wall
         normals set at initialisation: they are not stored (no read and write of them per
         node and step) and the lattice copies them into the other snapshot once before an

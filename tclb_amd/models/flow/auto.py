@@ -95,9 +95,11 @@ def build(q19: bool = False, part: bool = False, coll: str = "MRT", fmt: bool = 
     if part:
         m.add_stage("BaseIteration", "Run", save_fields=["f"], load_densities=["f", "Force"])
         m.add_stage("BaseInit", "Init", save_fields=["f", "Force"])
-        # the densities are pulled only on the nodes a particle covers (auto.inc CalcF)
+        # the densities are pulled only on the nodes a particle covers (auto.inc CalcF);
+        # on the GPU those nodes run in a deferred kernel of their own (split + defer), so
+        # the zero-force pass over the rest of the lattice keeps a small register budget
         m.add_stage("CalcF", "CalcF", save_fields=["Force"], load_densities=["f"], particle=True,
-                    lazy_load=True)
+                    lazy_load=True, split=True, defer=True)
         m.add_action("Iteration", ["BaseIteration", "CalcF"])
         m.add_action("Init", ["BaseInit", "CalcF"])
     else:

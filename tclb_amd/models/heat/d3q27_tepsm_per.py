@@ -90,7 +90,9 @@ def build(nebb: bool = False, sup: bool = False, isothermal: bool = False) -> Mo
     m.add_stage("BaseIteration", "Run", save_fields=groups, load_densities=groups, split=True,
                 defer=not isothermal)
     # lazy: the populations are pulled only where a particle covers the node
-    m.add_stage("CalcF", "CalcF", save_fields=["Force"], load_densities=calc_load, particle=True, lazy_load=True)
+    # (split + defer: the covered nodes' force pass is a kernel of its own on the GPU)
+    m.add_stage("CalcF", "CalcF", save_fields=["Force"], load_densities=calc_load, particle=True, lazy_load=True,
+                split=True, defer=True)
     m.add_action("Iteration", ["BaseIteration", "CalcF"])
     m.add_action("Init", ["BaseInit", "CalcF"])
     m.add_node_type("Solid", "BOUNDARY")

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """The part256 force stage with the particle changed (tools/bench_configs.py part256):
 radius (default n/16) and position, to separate the cost of the nodes a particle covers
-from the whole-lattice pass (profiles/README.md r06j).  Run under rocprofv3 --kernel-trace.
+from the whole-lattice pass (profiles/README.md r06k-l).  Run under rocprofv3 --kernel-trace.
 
     python tools/calcf_probe.py --radius 2 --steps 20
 """
