@@ -78,6 +78,63 @@ def alternate_actions(lat, steps):
         lat.iterate(1, glob_last=False, action="TempToSteadyState")
 
 
+def particle_case(shape, steps, comm):
+    """the config-5 model (auto_d3q19_part, tools/bench_configs.py part256) with three
+    density-2 spheres placed to cross z-slab boundaries: one straddling the middle cut, one
+    wrapping the periodic z = 0 plane, one moving in z so it changes owner rank during the
+    run.  Forces are summed over the ranks, positions advanced by SimplePart"""
+    from tclb_amd.lattice import Lattice
+    from tclb_amd.particles import SimplePart
+    nx, ny, nz = shape
+    lat = Lattice("auto_d3q19_part", shape, comm=comm)
+    fl = np.full((lat.NZ, lat.NY, nx), lat.model.node_type("MRT").value, dtype=np.uint32)
+    lat.set_flags(fl)
+    lat.set_setting("Viscosity", 0.05)
+    lat.set_setting("ForceX", 1e-5)
+    ps = SimplePart()
+    r = 3.0
+    m = 2.0 * 4.0 / 3.0 * np.pi * r ** 3
+    ps.add(x=(nx / 2, ny / 2, nz / 2 + 0.3), r=r, v=(0.02, 0, 0), m=m)
+    ps.add(x=(nx / 4 + 0.4, ny / 4, 0.7), r=r, v=(0, 0.01, -0.02), m=m)
+    ps.add(x=(3 * nx / 4, 3 * ny / 4, nz / 4 - 1.2), r=r, v=(0, 0, 0.4), m=m)
+    ps.periodic[:] = True
+    ps.period[:] = shape
+    lat.particles = ps
+    lat.init()
+    lat.iterate(steps)
+    return lat
+
+
+def worker_particles(rank, world, port, shape, steps, out):
+    """particle_case on `world` gloo ranks through the native loop, sends and receives
+    paired by issue order (TCLB_DIST_ORDER_MATCH from the parent)"""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    os.environ["TCLB_DIST_NATIVE"] = "1"
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from tclb_amd.parallel.comm import TorchDistComm
+    comm = TorchDistComm()
+    lat = particle_case(shape, steps, comm)
+    ps = lat.particles
+    parts = comm.gather_objects((lat.slab.offset, lat.fields_interior().numpy(), lat._native_path("Iteration"),
+                                 lat._dist.transport if lat._dist is not None else None,
+                                 np.asarray(ps.x, dtype=float), np.asarray(ps.v, dtype=float),
+                                 np.asarray(ps.force, dtype=float)))
+    if rank == 0:
+        gnx, gny, gnz = lat.gshape
+        full = np.zeros((lat.nf, gnz, gny, gnx))
+        for (ox, oy, oz), a, *_ in parts:
+            full[:, oz:oz + a.shape[1], oy:oy + a.shape[2], :] = a
+        np.save(out, full)
+        np.savez(out + ".part.npz", x=np.stack([p[4] for p in parts]), v=np.stack([p[5] for p in parts]),
+                 force=np.stack([p[6] for p in parts]))
+        import json
+        with open(out + ".json", "w") as f:
+            json.dump({"path": [p[2] for p in parts], "transport": [p[3] for p in parts]}, f)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
 def worker_catalog(rank, world, port, model, steps, out, overlap, mirror="1", alternate=False):
     """any catalog model with the generic set-up of tests/model_cases.py (global-coordinate
     perturbation), gathered to rank 0 as in worker()"""

@@ -160,6 +160,31 @@ def test_grid_alternating_actions(tmp_path, monkeypatch):
     assert np.array_equal(np.load(out), ref.fields_interior().numpy())
 
 
+def test_native_particles_four_ranks_issue_order(tmp_path, monkeypatch):
+    """config 5's model on 4 z-slab ranks through the native loop (particle stages in the
+    loop, forces all-reduced), sends and receives paired by issue order as RCCL pairs them:
+    three spheres straddle / wrap / move across the rank cuts.  Equals one rank to
+    rounding (the force sum's order differs), every rank runs the loop path"""
+    monkeypatch.setenv("TCLB_DIST_ORDER_MATCH", "1")
+    shape, steps = (16, 16, 24), 8
+    ref = dist_worker.particle_case(shape, steps, LoopbackComm())
+    out = str(tmp_path / "full.npy")
+    mp.start_processes(dist_worker.worker_particles, args=(4, _port(), shape, steps, out),
+                       nprocs=4, start_method="spawn", join=True)
+    meta = json.load(open(out + ".json"))
+    assert meta["path"] == ["loop"] * 4 and meta["transport"] == ["callback"] * 4
+    full = np.load(out)
+    r = ref.fields_interior().numpy()
+    assert np.allclose(full, r, rtol=0, atol=1e-12), np.abs(full - r).max()
+    p = np.load(out + ".part.npz")
+    px = np.asarray(ref.particles.x, dtype=float)
+    assert abs(px[2, 2] - (shape[2] / 4 - 1.2)) > 2.0          # the z mover changed rank
+    for k, want in (("x", px), ("v", np.asarray(ref.particles.v, dtype=float)),
+                    ("force", np.asarray(ref.particles.force, dtype=float))):
+        for rk in range(4):
+            assert np.allclose(p[k][rk], want, rtol=1e-9, atol=1e-12), (k, rk)
+
+
 def test_choose_grid_minimises_cut():
     from tclb_amd.parallel.decomp import choose_grid, decompose
     assert choose_grid(512, 512, 512, 8) in ((2, 4), (4, 2))
