@@ -54,6 +54,10 @@ rcclenv)
   step "slab rccl NCCL_NCHANNELS_PER_PEER=1" 300 $O/rcclenv_pp1.json env NCCL_NCHANNELS_PER_PEER=1 python bench.py --shape 512,512,64 --steps 200 --warmup 20 --loopback-dist --transport rccl
   step "slab ipc" 300 $O/rcclenv_ipc.json python bench.py --shape 512,512,64 --steps 200 --warmup 20 --loopback-dist --transport ipc
   step "slab copy" 300 $O/rcclenv_copy.json python bench.py --shape 512,512,64 --steps 200 --warmup 20 --loopback-dist --transport copy ;;
+r06r)
+  step "placement probe + IPC GPU tests" 400 $O/pytest_place_ipc.log python -u -m pytest tests/test_gpu_placement.py tests/test_gpu_ipc.py -v -m gpu --timeout 120 --timeout-method thread
+  step "bench half-shift" 300 $O/bench_half_shift.json python bench.py --precision half-shift
+  step "bench half" 300 $O/bench_half.json python bench.py --precision half ;;
 tests) step "gpu tests" 900 $O/pytest_gpu.log python -u -m pytest tests -v -m gpu --timeout 120 --timeout-method thread ;;
 bench)
   step "bench fp64" 300 $O/bench_fp64.json python bench.py

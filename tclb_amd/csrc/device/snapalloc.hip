@@ -101,7 +101,7 @@ __global__ void __launch_bounds__(256) k_probe(T* buf, T* sink, long long n, lon
     T s = 0;
 #pragma unroll
     for (int k = 0; k < K; k++) s += buf[k * stride + i];
-    if (s == (T)-1.2345e30) sink[0] = s;
+    if (s == (T)12345) sink[0] = s;
   } else {
 #pragma unroll
     for (int k = 0; k < K; k++) __builtin_nontemporal_store((T)0, buf + k * stride + i);
@@ -128,12 +128,14 @@ int probe(void* buf, void* sink, long long n, long long stride, int K, int op, h
 
 }  // namespace
 
-// op 1: read / op 2: write (zeros) of K planes of n elements (elem_bytes 8 or 4), stride apart
+// op 1: read / op 2: write (zeros) of K planes of n elements (elem_bytes 8, 4 or 2: the
+// half storage modes, probed as 16-bit words), stride apart
 extern "C" int tclb_snap_probe(void* buf, void* sink, long long n, long long stride, int K, int elem_bytes, int op,
                                void* stream) {
   if (n <= 0 || K <= 0 || (n + 255) / 256 > 0x7fffffffLL) return (int)hipErrorInvalidValue;
   if (elem_bytes == 8) return probe<double>(buf, sink, n, stride, K, op, (hipStream_t)stream);
   if (elem_bytes == 4) return probe<float>(buf, sink, n, stride, K, op, (hipStream_t)stream);
+  if (elem_bytes == 2) return probe<unsigned short>(buf, sink, n, stride, K, op, (hipStream_t)stream);
   return (int)hipErrorInvalidValue;
 }
 

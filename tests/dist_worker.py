@@ -78,7 +78,7 @@ def alternate_actions(lat, steps):
         lat.iterate(1, glob_last=False, action="TempToSteadyState")
 
 
-def particle_case(shape, steps, comm):
+def particle_case(shape, steps, comm, device=None):
     """the config-5 model (auto_d3q19_part, tools/bench_configs.py part256) with three
     density-2 spheres placed to cross z-slab boundaries: one straddling the middle cut, one
     wrapping the periodic z = 0 plane, one moving in z so it changes owner rank during the
@@ -86,7 +86,7 @@ def particle_case(shape, steps, comm):
     from tclb_amd.lattice import Lattice
     from tclb_amd.particles import SimplePart
     nx, ny, nz = shape
-    lat = Lattice("auto_d3q19_part", shape, comm=comm)
+    lat = Lattice("auto_d3q19_part", shape, comm=comm, **({"device": device} if device is not None else {}))
     fl = np.full((lat.NZ, lat.NY, nx), lat.model.node_type("MRT").value, dtype=np.uint32)
     lat.set_flags(fl)
     lat.set_setting("Viscosity", 0.05)

@@ -26,6 +26,8 @@ def run_case(case, shape, steps, comm, grid=None):
         lat.iterate(steps)
         return lat
     import dist_worker
+    if case == "part3":
+        return dist_worker.particle_case(shape, steps, comm, device=dev)
     from tclb_amd.lattice import Lattice
     lat = Lattice("d3q27", shape, comm=comm, grid=grid, device=dev)
     lat.set_flags(dist_worker.setup_flags(lat))

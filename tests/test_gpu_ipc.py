@@ -95,6 +95,26 @@ def test_ipc_particle_allreduce(tmp_path):
     assert float(np.abs(np.asarray(ps.force)).max()) > 0.0      # the coupling acts
 
 
+def test_ipc_particles_cross_ranks(tmp_path):
+    """4 processes on one GPU: three spheres straddle, wrap and cross the z-slab cuts
+    (tests/dist_worker.py particle_case); halos and the force all-reduce through IPC
+    inside the native loop equal one rank to rounding (atomic force sums)"""
+    shape, steps = (32, 32, 48), 8
+    ref = _ref("part3", shape, steps)
+    out = str(tmp_path / "full.npy")
+    _spawn(4, ("part3", shape, steps, out))
+    meta = json.load(open(out + ".json"))
+    assert meta["transport"] == ["ipc"] * 4
+    full = np.load(out)
+    r = ref.fields_interior().cpu().numpy()
+    assert np.abs(full - r).max() <= 1e-12 * np.abs(r).max()
+    ps = ref.particles
+    for key, val in (("x", ps.x), ("v", ps.v), ("force", ps.force)):
+        a, b = np.asarray(meta["part"][key]), np.asarray(val, dtype=float)
+        assert np.allclose(a, b, rtol=1e-9, atol=1e-13), (key, a, b)
+    assert float(np.abs(np.asarray(ps.force)).max()) > 0.0
+
+
 def test_ipc_loopback_one_rank(monkeypatch):
     """one process pulling from itself through the same IPC code (no peer to map) equals
     the plain one-rank lattice bit for bit"""
