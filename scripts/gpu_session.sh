@@ -54,6 +54,22 @@ rcclenv)
   step "slab rccl NCCL_NCHANNELS_PER_PEER=1" 300 $O/rcclenv_pp1.json env NCCL_NCHANNELS_PER_PEER=1 python bench.py --shape 512,512,64 --steps 200 --warmup 20 --loopback-dist --transport rccl
   step "slab ipc" 300 $O/rcclenv_ipc.json python bench.py --shape 512,512,64 --steps 200 --warmup 20 --loopback-dist --transport ipc
   step "slab copy" 300 $O/rcclenv_copy.json python bench.py --shape 512,512,64 --steps 200 --warmup 20 --loopback-dist --transport copy ;;
+c2probe)
+  # the r05m class-2 fault against one backend stage at a time (build.py c2w0_* variants)
+  for v in ${C2VARIANTS:-c2w0 c2w0_noagpr c2w0_nomisched c2w0_nopostra c2w0_nohrp c2w0_o1 c2w0_verify}; do
+    step "split probe $v" 300 $O/c2probe_$v.log env MODE=noglob STEPS=1 VARIANT=$v python tools/split_probe.py d3q27_tePSM_per_NEBB
+  done ;;
+c2old)
+  # the same probe on a checkout of the source in which the fault was found (git worktree
+  # _wt_c2 of 2088283, before the deferring stages changed the class-2 kernel)
+  for v in ${C2VARIANTS:-c2w0 c2w0_noagpr c2w0_nomisched c2w0_nopostra c2w0_nohrp c2w0_o1}; do
+    step "old-source split probe $v" 300 $O/c2old_$v.log bash -c "cd $R/_wt_c2 && MODE=noglob STEPS=1 VARIANT=$v python tools/split_probe.py d3q27_tePSM_per_NEBB"
+  done ;;
+adsched)
+  # the row-form k_ad fault (r05i-j) under the two scheduler switches that clear the class-2 one
+  for v in row_w2 row_w2_nohrp row_w2_nomisched ""; do
+    step "adjoint diag variant '$v'" 300 $O/adsched_${v:-default}.log env TCLB_AD_VARIANT=$v TCLB_NO_BUILD=1 python tools/adjoint_diag.py --repeats 1 --modes dual
+  done ;;
 r06r)
   step "placement probe + IPC GPU tests" 400 $O/pytest_place_ipc.log python -u -m pytest tests/test_gpu_placement.py tests/test_gpu_ipc.py -v -m gpu --timeout 120 --timeout-method thread
   step "bench half-shift" 300 $O/bench_half_shift.json python bench.py --precision half-shift

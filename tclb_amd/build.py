@@ -64,6 +64,16 @@ VARIANTS = {
     "tw8": ["-DTCLB_NT_STORE=1", "-DTCLB_TILE_WAVES=8"],
     # class-2 kernels without their 2-wave floor (reproduces the r05m tePSM fault)
     "c2w0": ["-DTCLB_NT_STORE=1", "-DTCLB_SPLIT_WAVES2=0"],
+    # the same form with one backend stage changed at a time (which stage the fault needs):
+    # VGPR->AGPR spill copies off, machine schedulers off, the high-pressure reschedule off,
+    # -O1, and the machine verifier after every codegen pass
+    "c2w0_noagpr": ["-DTCLB_NT_STORE=1", "-DTCLB_SPLIT_WAVES2=0", "-mllvm", "-amdgpu-spill-vgpr-to-agpr=0"],
+    "c2w0_nomisched": ["-DTCLB_NT_STORE=1", "-DTCLB_SPLIT_WAVES2=0", "-mllvm", "-enable-misched=0"],
+    "c2w0_nopostra": ["-DTCLB_NT_STORE=1", "-DTCLB_SPLIT_WAVES2=0", "-mllvm", "-enable-post-misched=0"],
+    "c2w0_nohrp": ["-DTCLB_NT_STORE=1", "-DTCLB_SPLIT_WAVES2=0", "-mllvm",
+                   "-amdgpu-disable-unclustered-high-rp-reschedule"],
+    "c2w0_o1": ["-DTCLB_NT_STORE=1", "-DTCLB_SPLIT_WAVES2=0", "-O1"],
+    "c2w0_verify": ["-DTCLB_NT_STORE=1", "-DTCLB_SPLIT_WAVES2=0", "-mllvm", "-verify-machineinstrs"],
     "cw2": ["-DTCLB_NT_STORE=1", "-DTCLB_SPLIT_WAVES=2"],
     "cw3": ["-DTCLB_NT_STORE=1", "-DTCLB_SPLIT_WAVES=3"],
     "cw4": ["-DTCLB_NT_STORE=1", "-DTCLB_SPLIT_WAVES=4"],
@@ -98,7 +108,13 @@ AD_VARIANTS.update({"row": ["-DTCLB_FLAT_NODE=0"], "row_o1": ["-DTCLB_FLAT_NODE=
                                       "-amdgpu-spill-vgpr-to-agpr=0"],
                     "row_w2_wpe2": ["-DTCLB_FLAT_NODE=0", "-DTCLB_AD_WINDOW=2", "-DTCLB_AD_WAVES=2"],
                     "row_wpe2": ["-DTCLB_FLAT_NODE=0", "-DTCLB_AD_WAVES=2"],
-                    "flat_wpe2": ["-DTCLB_AD_WAVES=2"]})
+                    "flat_wpe2": ["-DTCLB_AD_WAVES=2"],
+                    # round 6: the primal class-2 fault needs the scheduler's unclustered
+                    # high-pressure reschedule stage (profiles/README.md r06s-t); the same
+                    # two switches on the failing row form
+                    "row_w2_nohrp": ["-DTCLB_FLAT_NODE=0", "-DTCLB_AD_WINDOW=2", "-mllvm",
+                                     "-amdgpu-disable-unclustered-high-rp-reschedule"],
+                    "row_w2_nomisched": ["-DTCLB_FLAT_NODE=0", "-DTCLB_AD_WINDOW=2", "-mllvm", "-enable-misched=0"]})
 
 
 def ad_variant_flags(variant: str) -> Optional[List[str]]:
