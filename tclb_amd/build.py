@@ -74,6 +74,8 @@ VARIANTS = {
                    "-amdgpu-disable-unclustered-high-rp-reschedule"],
     "c2w0_o1": ["-DTCLB_NT_STORE=1", "-DTCLB_SPLIT_WAVES2=0", "-O1"],
     "c2w0_verify": ["-DTCLB_NT_STORE=1", "-DTCLB_SPLIT_WAVES2=0", "-mllvm", "-verify-machineinstrs"],
+    # the default build with the scheduler's high-pressure reschedule stage off (perf A/B)
+    "nohrp": ["-DTCLB_NT_STORE=1", "-mllvm", "-amdgpu-disable-unclustered-high-rp-reschedule"],
     "cw2": ["-DTCLB_NT_STORE=1", "-DTCLB_SPLIT_WAVES=2"],
     "cw3": ["-DTCLB_NT_STORE=1", "-DTCLB_SPLIT_WAVES=3"],
     "cw4": ["-DTCLB_NT_STORE=1", "-DTCLB_SPLIT_WAVES=4"],
