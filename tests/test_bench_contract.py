@@ -36,6 +36,23 @@ def test_bench_two_ranks_json_line():
         assert out["metric"] == metric
 
 
+def test_bench_eight_ranks_like_the_scaling_run():
+    """the driver's 8-GPU command line (torch.distributed.run, 8 ranks, --gpus 8) on gloo
+    ranks: 32 z planes over 8 slabs of 4, every physics check on, one JSON line"""
+    env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=8",
+           "--master-addr", "127.0.0.1", "--master-port", "29617", os.path.join(ROOT, "bench.py"),
+           "--cpu", "--size", "32", "--steps", "3", "--warmup", "1", "--gpus", "8"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 8 and out["config"]["parallelism"] == "zslab8"
+    assert out["config"]["lattice"] == [32, 32, 32] and out["scaling"] == "strong"
+    assert all(out["checks"][k] for k in ("mass_ok", "z_invariant", "x_invariant", "collides"))
+
+
 def test_bench_spawns_its_own_ranks():
     """--gpus N without a launcher starts N ranks itself (torch.distributed.run as a child
     process): the line reports n_gpus = N, never a silent 1-rank run; the ranks step
