@@ -70,6 +70,13 @@ adsched)
   for v in row_w2 row_w2_nohrp row_w2_nomisched ""; do
     step "adjoint diag variant '$v'" 300 $O/adsched_${v:-default}.log env TCLB_AD_VARIANT=$v TCLB_NO_BUILD=1 python tools/adjoint_diag.py --repeats 1 --modes dual
   done ;;
+final6)
+  # round-6 closing evidence: every BASELINE config on the final tree, hardware counters
+  # of the headline fp64 kernel, part256 and the tePSM collide
+  step "configs" 500 $O/configs.log python tools/bench_configs.py
+  step "counters d3q27 fp64" 500 $O/counters_d3q27_fp64.log python tools/counters.py --tag d3q27_512_fp64 --nodes 134217728 --outdir $O/counters -- python3 $R/bench.py --steps 5 --warmup 1
+  step "counters part256" 500 $O/counters_part256.log python tools/counters.py --tag part256_fp64 --nodes 16777216 --outdir $O/counters -- python3 $R/tools/bench_configs.py --configs part256 --steps 5 --warmup 1
+  step "counters tePSM 256" 500 $O/counters_tepsm.log python tools/counters.py --tag tepsm_256_fp64 --nodes 16777216 --outdir $O/counters -- python3 $R/tools/perf_models.py --models d3q27_tePSM_per_NEBB --n3 256 --steps 5 ;;
 r06r)
   step "placement probe + IPC GPU tests" 400 $O/pytest_place_ipc.log python -u -m pytest tests/test_gpu_placement.py tests/test_gpu_ipc.py -v -m gpu --timeout 120 --timeout-method thread
   step "bench half-shift" 300 $O/bench_half_shift.json python bench.py --precision half-shift

@@ -27,7 +27,13 @@ from tclb_amd.utils.guard import collision_check  # noqa: E402
 
 
 def _time(lat, steps, warmup, glob_every=False):
-    lat.iterate(warmup, glob_last=False)
+    # the warm-up runs the timed sequence's kernels, the globals step included (the first
+    # launch of a kernel instantiation is not part of a steady-state step)
+    if glob_every:
+        for _ in range(warmup):
+            lat.iterate(1, glob_last=True, reduce=False)
+    else:
+        lat.iterate(warmup, glob_last=True)
     torch.cuda.synchronize()
     t = time.perf_counter()
     if glob_every:        # globals integrated on every step (a <Log Iterations="1"> case)
