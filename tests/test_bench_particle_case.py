@@ -28,3 +28,27 @@ def test_part256_case_stays_bounded():
     assert chk["globals_finite"] and chk["fields_finite"] and chk["particle_bounded"], chk
     assert chk["collides"], chk
     assert lat._native_path("Iteration") == "loop"          # particle stages in the native loop
+
+
+class _Rec:
+    """records the iterate calls of the timing helper"""
+
+    def __init__(self):
+        self.calls = []
+
+    def iterate(self, n, glob_last=True, reduce=True):
+        self.calls.append((n, glob_last))
+
+
+def test_config_warmup_runs_the_globals_step(monkeypatch):
+    """bench_configs' warm-up runs the timed sequence, the globals step included, so the
+    window never holds the first launch of the globals kernel (r06x: that launch cut the
+    20-step cavity from ~18 000 to 14 626 MLUPS)"""
+    import bench_configs as bc
+    monkeypatch.setattr(torch.cuda, "synchronize", lambda *a, **k: None)
+    lat = _Rec()
+    bc._time(lat, 20, 3)
+    assert lat.calls == [(3, True), (20, True)]
+    lat = _Rec()
+    bc._time(lat, 2, 2, glob_every=True)
+    assert lat.calls == [(1, True)] * 4
